@@ -1,0 +1,127 @@
+"""Loader for libfedagg.so, the HIP (gfx950) C-ABI declared in include/fedagg.h.
+
+The library is linked against ``libamdhip64.so.7``.  PyTorch-ROCm ships its own
+HIP runtime with the same soname, so torch MUST be imported first: the dynamic
+linker then resolves our NEEDED entry to torch's already-loaded runtime and the
+device pointers / hipStream_t handles torch hands us are valid in our calls.
+Loading the library before torch would map a second HIP runtime; we check for
+that and refuse.
+
+There is deliberately no fallback: if the library is missing or cannot be
+loaded, every product entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
+
+_LIB_NAME = "libfedagg.so"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
+
+# Must match include/fedagg.h
+ABI_VERSION = 1
+FEDAGG_INIT = 0x1
+FEDAGG_FINALIZE = 0x2
+FEDAGG_NT = 0x4
+FEDAGG_SCALAR = 0x8
+FEDAGG_UNROLL_SHIFT = 8
+FEDAGG_VPT_SHIFT = 12
+FEDAGG_EINVAL = -22
+
+# (name, restype, argtypes) for every symbol include/fedagg.h declares.
+_c_float_p = ctypes.c_void_p
+SIGNATURES = {
+    "fedagg_abi_version": (ctypes.c_int, []),
+    "fedagg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "fedagg_reduce_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+         ctypes.c_int, ctypes.c_void_p],
+    ),
+    "fedagg_reduce_rows_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
+         ctypes.c_void_p],
+    ),
+    "fedagg_finalize_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p,
+         ctypes.c_void_p],
+    ),
+    "fedagg_fedavg_sgd_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_int64, ctypes.c_void_p],
+    ),
+    "fedagg_adabest_sgd_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p],
+    ),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class FedAggError(RuntimeError):
+    """A libfedagg call returned a non-zero status."""
+
+
+def _hip_runtimes_mapped():
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return paths
+
+
+def load():
+    """Load (once) and return the ctypes handle; raise if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise FedAggError(
+                f"{LIB_PATH} not found: build it with `python -c "
+                f"'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
+            )
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.fedagg_abi_version() != ABI_VERSION:
+            raise FedAggError("libfedagg ABI version mismatch; rebuild the library")
+        runtimes = _hip_runtimes_mapped()
+        if len(runtimes) > 1:
+            raise FedAggError(
+                "two HIP runtimes are mapped (%s); import torch before fedsim_amd"
+                % sorted(runtimes)
+            )
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().fedagg_strerror(rc).decode()
+        raise FedAggError(f"{what} failed ({rc}): {msg}")
+
+
+def exported_symbols():
+    """Names of the C-ABI entry points (the ones include/fedagg.h declares)."""
+    return list(SIGNATURES)

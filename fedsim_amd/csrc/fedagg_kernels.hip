@@ -1,0 +1,448 @@
+// fedagg_kernels.hip — MI355X (gfx950 / CDNA4) kernels for FedSim's server
+// aggregation hot path, exported through the C-ABI in include/fedagg.h.
+//
+// What the reference does (pure Python + PyTorch CPU):
+//   serial_aggregation   fedsim/distributed/centralized/training/utils.py:34-46
+//     -> SerialAggregator.add  fedsim/utils/aggregators.py:23-40
+//        new_v = value * weight          (fp32 tensor x Python scalar -> fl32(w))
+//        sum_v = sum_v + new_v           (starts from the int 0)
+//   SerialAggregator.pop  fedsim/utils/aggregators.py:104-122  -> v / w
+//   FedAvg.optimize       fedsim/distributed/centralized/training/fedavg.py:193-208
+//   AdaBest.optimize      fedsim/distributed/centralized/training/adabest.py:172-189
+//
+// Design (MI355X-first, not a translation — the reference has no kernels):
+//   * The reduction is HBM-bound (0.5 flop/byte, no MFMA).  Every client row is
+//     streamed exactly once: each lane owns VPT f32x4 column slots and walks
+//     the K client rows in arrival order, so each wave-instruction reads a
+//     contiguous 1 KiB run of a row and the running sum never leaves VGPRs.
+//   * Exact mode keeps the reference's per-column order k = 0..K-1 and its
+//     rounding (separate mul and add, no contraction, IEEE true division), so
+//     outputs are bit-identical to the reference CPU aggregation.
+//   * The per-client weight is wave-uniform: it is read with scalar loads
+//     (s_load through the scalar cache, broadcast from SGPRs) — the CDNA way to
+//     broadcast a uniform value, cheaper than an LDS round trip.
+//   * k is unrolled U-deep: U*VPT independent 16-byte loads are issued before
+//     the in-order adds consume them, so each wave keeps U*VPT KiB in flight.
+//   * The row base is uniform (SGPR pair) and the per-lane offset is 32-bit,
+//     which lets the compiler use global_load_dwordx4 v, v_off, s[base:base+1].
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
+// (see __graft_entry__.build()).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fedagg.h"
+
+// The reference rounds every product and every sum separately; forbid the
+// compiler from fusing them into an FMA anywhere in this translation unit.
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+// Native clang vector (HIP's float4 is a struct and cannot feed the
+// nontemporal builtin).
+using f32x4 = float __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// Row addressing policies
+// ---------------------------------------------------------------------------
+struct RowsStrided {
+  const float* X;
+  int64_t ldx;
+  __device__ __forceinline__ const char* row(int64_t k) const {
+    return reinterpret_cast<const char*>(X + k * ldx);
+  }
+};
+
+struct RowsTable {
+  const float* const* rows;
+  __device__ __forceinline__ const char* row(int64_t k) const {
+    return reinterpret_cast<const char*>(rows[k]);
+  }
+};
+
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const char* base, uint32_t off) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(base + off);
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ float ld1(const char* base, uint32_t off) {
+  const float* p = reinterpret_cast<const float*>(base + off);
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+// acc = fl32(acc + fl32(x * w)) — two roundings, as ATen CPU mul then add.
+__device__ __forceinline__ float axpy_rn(float acc, float x, float w) {
+  const float prod = x * w;
+  return acc + prod;
+}
+
+__device__ __forceinline__ f32x4 axpy_rn4(f32x4 a, f32x4 x, float w) {
+  a.x = axpy_rn(a.x, x.x, w);
+  a.y = axpy_rn(a.y, x.y, w);
+  a.z = axpy_rn(a.z, x.z, w);
+  a.w = axpy_rn(a.w, x.w, w);
+  return a;
+}
+
+__device__ __forceinline__ f32x4 div4(f32x4 a, float d) {
+  // correctly rounded IEEE division (hipcc default
+  // -fhip-fp32-correctly-rounded-divide-sqrt); NOT a * (1/d).
+  a.x = a.x / d;
+  a.y = a.y / d;
+  a.z = a.z / d;
+  a.w = a.w / d;
+  return a;
+}
+
+// ---------------------------------------------------------------------------
+// Exact-mode reduction, f32x4 slots.
+//   slot s covers columns [4s, 4s+4).  Block b owns slots
+//   [b*256*VPT, (b+1)*256*VPT); lane t of the block owns s = base + j*256 + t
+//   for j < VPT, so every wave-instruction touches 64 consecutive slots (1 KiB).
+// ---------------------------------------------------------------------------
+template <int U, int VPT, bool NT, bool GUARD, class Rows>
+__device__ __forceinline__ void reduce_vec_body(const Rows& rows,
+                                                const float* __restrict__ w,
+                                                int64_t B, int64_t nvec,
+                                                const float* acc_in, float* out,
+                                                float W32, int flags) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * (kBlock * VPT) + threadIdx.x;
+  uint32_t off[VPT];
+  bool ok[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    int64_t s = base + j * kBlock;
+    ok[j] = GUARD ? (s < nvec) : true;
+    if (GUARD && !ok[j]) s = nvec - 1;  // clamp: load something valid, store nothing
+    off[j] = static_cast<uint32_t>(s) * 16u;
+  }
+
+  f32x4 a[VPT];
+  if (flags & FEDAGG_INIT) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+      a[j] = ld4<false>(reinterpret_cast<const char*>(acc_in), off[j]);
+  }
+
+  int64_t k = 0;
+  for (; k + U <= B; k += U) {
+    f32x4 v[U][VPT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const char* r = rows.row(k + u);
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) v[u][j] = ld4<NT>(r, off[j]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wk = w[k + u];
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], v[u][j], wk);
+    }
+  }
+  for (; k < B; ++k) {
+    const char* r = rows.row(k);
+    const float wk = w[k];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], ld4<NT>(r, off[j]), wk);
+  }
+
+  if (flags & FEDAGG_FINALIZE) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) a[j] = div4(a[j], W32);
+  }
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    if (ok[j]) *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(out) + off[j]) = a[j];
+  }
+}
+
+// Scalar columns [col0, col0 + ncols): the P % 4 tail of the f32x4 path.
+template <bool NT, class Rows>
+__device__ __forceinline__ void reduce_scalar_cols(const Rows& rows,
+                                                   const float* __restrict__ w,
+                                                   int64_t B, int64_t col,
+                                                   const float* acc_in, float* out,
+                                                   float W32, int flags) {
+  const uint32_t off = static_cast<uint32_t>(col) * 4u;
+  float a = (flags & FEDAGG_INIT) ? 0.f : acc_in[col];
+  for (int64_t k = 0; k < B; ++k) a = axpy_rn(a, ld1<NT>(rows.row(k), off), w[k]);
+  if (flags & FEDAGG_FINALIZE) a = a / W32;
+  out[col] = a;
+}
+
+template <int U, int VPT, bool NT, class Rows>
+__global__ __launch_bounds__(kBlock) void k_reduce_vec(Rows rows,
+                                                       const float* __restrict__ w,
+                                                       int64_t B, int64_t nvec,
+                                                       int tail, const float* acc_in,
+                                                       float* out, float W32,
+                                                       int flags) {
+  const int64_t block_end = static_cast<int64_t>(blockIdx.x + 1) * (kBlock * VPT);
+  if (block_end <= nvec) {
+    reduce_vec_body<U, VPT, NT, false>(rows, w, B, nvec, acc_in, out, W32, flags);
+  } else {
+    if (nvec > 0)
+      reduce_vec_body<U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
+    // The last block also owns the (P % 4) scalar tail columns.
+    if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
+      reduce_scalar_cols<NT>(rows, w, B, nvec * 4 + threadIdx.x, acc_in, out, W32, flags);
+  }
+}
+
+// Generic path for rows that are not 16-byte aligned: one column per lane,
+// 4-byte coalesced loads (256 B per wave-instruction).  Same arithmetic.
+template <class Rows>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(Rows rows,
+                                                          const float* __restrict__ w,
+                                                          int64_t B, int64_t P,
+                                                          const float* acc_in,
+                                                          float* out, float W32,
+                                                          int flags) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (c >= P) return;
+  reduce_scalar_cols<false>(rows, w, B, c, acc_in, out, W32, flags);
+}
+
+// ---------------------------------------------------------------------------
+// Elementwise epilogues (grid-stride, f32x4 body + scalar tail).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_finalize(const float* acc, float W32,
+                                                     int64_t P, float* out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t nvec = P / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec; i += stride) {
+    f32x4 a = reinterpret_cast<const f32x4*>(acc)[i];
+    reinterpret_cast<f32x4*>(out)[i] = div4(a, W32);
+  }
+  if (blockIdx.x == 0 && static_cast<int64_t>(threadIdx.x) < P - nvec * 4) {
+    const int64_t c = nvec * 4 + threadIdx.x;
+    out[c] = acc[c] / W32;
+  }
+}
+
+// torch CPU SGD.step = param.add_(grad, alpha=-lr) = fma(-lr, g, param)
+__device__ __forceinline__ float sgd_rn(float c, float g, float neg_lr) {
+  return __builtin_fmaf(neg_lr, g, c);
+}
+
+__device__ __forceinline__ void fedavg_elem(const float* avg, float neg_lr, float* cloud,
+                                            float* grad_out, int64_t i) {
+  const float c = cloud[i];
+  const float g = c - avg[i];
+  if (grad_out) grad_out[i] = g;
+  cloud[i] = sgd_rn(c, g, neg_lr);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fedavg_sgd(const float* __restrict__ avg,
+                                                       float neg_lr,
+                                                       float* __restrict__ cloud,
+                                                       float* __restrict__ grad_out,
+                                                       int64_t P) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t nvec = P / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec; i += stride) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(avg)[i];
+    f32x4 c = reinterpret_cast<f32x4*>(cloud)[i];
+    f32x4 g;
+    g.x = c.x - a.x; g.y = c.y - a.y; g.z = c.z - a.z; g.w = c.w - a.w;
+    if (grad_out) reinterpret_cast<f32x4*>(grad_out)[i] = g;
+    c.x = sgd_rn(c.x, g.x, neg_lr); c.y = sgd_rn(c.y, g.y, neg_lr);
+    c.z = sgd_rn(c.z, g.z, neg_lr); c.w = sgd_rn(c.w, g.w, neg_lr);
+    reinterpret_cast<f32x4*>(cloud)[i] = c;
+  }
+  if (blockIdx.x == 0 && static_cast<int64_t>(threadIdx.x) < P - nvec * 4)
+    fedavg_elem(avg, neg_lr, cloud, grad_out, nvec * 4 + threadIdx.x);
+}
+
+__device__ __forceinline__ void adabest_elem(const float* avg, float beta, float neg_lr,
+                                             float* cloud, float* avg_prev, float* grad_out,
+                                             int64_t i) {
+  const float a = avg[i];
+  const float h = beta * (avg_prev[i] - a);
+  const float nw = a - h;
+  const float c = cloud[i];
+  const float g = c - nw;
+  if (grad_out) grad_out[i] = g;
+  cloud[i] = sgd_rn(c, g, neg_lr);
+  avg_prev[i] = a;
+}
+
+__global__ __launch_bounds__(kBlock) void k_adabest_sgd(const float* __restrict__ avg,
+                                                        float beta, float neg_lr,
+                                                        float* __restrict__ cloud,
+                                                        float* __restrict__ avg_prev,
+                                                        float* __restrict__ grad_out,
+                                                        int64_t P) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < P; i += stride)
+    adabest_elem(avg, beta, neg_lr, cloud, avg_prev, grad_out, i);
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline int elementwise_grid(int64_t n) {
+  int64_t g = (n + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > 256 * 8) g = 256 * 8;  // 8 blocks per CU, grid-stride the rest
+  return static_cast<int>(g);
+}
+
+template <int U, int VPT, bool NT, class Rows>
+hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
+                      const float* acc_in, float* out, float W32, int flags,
+                      hipStream_t s) {
+  const int64_t nvec = P / 4;
+  const int tail = static_cast<int>(P - nvec * 4);
+  int64_t grid = (nvec + kBlock * VPT - 1) / (kBlock * VPT);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((k_reduce_vec<U, VPT, NT, Rows>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kBlock), 0, s, rows, w, B, nvec, tail, acc_in, out, W32, flags);
+  return hipGetLastError();
+}
+
+template <int VPT, bool NT, class Rows>
+hipError_t dispatch_unroll(int unroll_sel, const Rows& rows, const float* w, int64_t B,
+                           int64_t P, const float* acc_in, float* out, float W32,
+                           int flags, hipStream_t s) {
+  switch (unroll_sel) {
+    case 1: return launch_vec<4, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 3: return launch_vec<16, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 0:
+    case 2:
+    default: return launch_vec<8, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+  }
+}
+
+template <class Rows>
+hipError_t dispatch_reduce(const Rows& rows, bool vec_ok, const float* w, int64_t B,
+                           int64_t P, const float* acc_in, float* out, float W32,
+                           int flags, hipStream_t s) {
+  if (!vec_ok) {
+    int64_t grid = (P + kBlock - 1) / kBlock;
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL((k_reduce_scalar<Rows>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+                       0, s, rows, w, B, P, acc_in, out, W32, flags);
+    return hipGetLastError();
+  }
+  const int unroll_sel = (flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT;
+  const int vpt_sel = (flags & FEDAGG_VPT_MASK) >> FEDAGG_VPT_SHIFT;
+  const bool nt = (flags & FEDAGG_NT) != 0;
+  if (vpt_sel == 2) {
+    return nt ? dispatch_unroll<2, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+              : dispatch_unroll<2, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+  }
+  return nt ? dispatch_unroll<1, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+            : dispatch_unroll<1, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+}
+
+int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
+                      const float* out, int flags) {
+  if (B < 0 || P < 0) return FEDAGG_EINVAL;
+  if (P > (int64_t(1) << 30)) return FEDAGG_EINVAL;  // 32-bit per-row byte offsets
+  if (P == 0) return 0;
+  if (!out) return FEDAGG_EINVAL;
+  if (B > 0 && !w) return FEDAGG_EINVAL;
+  if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
+  if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
+                FEDAGG_VPT_MASK))
+    return FEDAGG_EINVAL;
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int fedagg_abi_version(void) { return FEDAGG_ABI_VERSION; }
+
+const char* fedagg_strerror(int code) {
+  if (code == 0) return "success";
+  if (code == FEDAGG_EINVAL) return "fedagg: invalid argument";
+  if (code == FEDAGG_EALIGN) return "fedagg: misaligned pointer";
+  if (code > 0) return hipGetErrorString(static_cast<hipError_t>(code));
+  return "fedagg: unknown error";
+}
+
+int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B, int64_t P,
+                      const float* acc_in, float* out, float W32, int flags, void* stream) {
+  int rc = check_reduce_args(w, B, P, acc_in, out, flags);
+  if (rc != 0 || P == 0) return rc;
+  if (B > 0 && (!X || ldx < P)) return FEDAGG_EINVAL;
+  const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(X) && (ldx % 4 == 0) &&
+                      aligned16(out) && ((flags & FEDAGG_INIT) || aligned16(acc_in));
+  RowsStrided rows{X, ldx};
+  return static_cast<int>(dispatch_reduce(rows, vec_ok, w, B, P, acc_in, out, W32, flags,
+                                          static_cast<hipStream_t>(stream)));
+}
+
+int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, int64_t P,
+                           const float* acc_in, float* out, float W32, int flags,
+                           void* stream) {
+  int rc = check_reduce_args(w, B, P, acc_in, out, flags);
+  if (rc != 0 || P == 0) return rc;
+  if (B > 0 && !rows) return FEDAGG_EINVAL;
+  // The table lives in device memory and cannot be inspected here without a
+  // sync: the caller passes FEDAGG_SCALAR unless every rows[k] is 16-B aligned.
+  const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(out) &&
+                      ((flags & FEDAGG_INIT) || aligned16(acc_in));
+  RowsTable tab{rows};
+  return static_cast<int>(dispatch_reduce(tab, vec_ok, w, B, P, acc_in, out, W32, flags,
+                                          static_cast<hipStream_t>(stream)));
+}
+
+int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out, void* stream) {
+  if (P < 0) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!acc || !out || !aligned16(acc) || !aligned16(out)) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_finalize, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), acc, W32, P, out);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_fedavg_sgd_f32(const float* avg, float lr, float* cloud, float* grad_out,
+                          int64_t P, void* stream) {
+  if (P < 0) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!avg || !cloud || !aligned16(avg) || !aligned16(cloud)) return FEDAGG_EINVAL;
+  if (grad_out && !aligned16(grad_out)) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_fedavg_sgd, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), avg, -lr, cloud, grad_out, P);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_adabest_sgd_f32(const float* avg, float beta, float lr, float* cloud,
+                           float* avg_prev, float* grad_out, int64_t P, void* stream) {
+  if (P < 0) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!avg || !cloud || !avg_prev) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_adabest_sgd, dim3(elementwise_grid(P)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), avg, beta, -lr, cloud, avg_prev,
+                     grad_out, P);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

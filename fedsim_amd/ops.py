@@ -1,0 +1,203 @@
+"""Typed Python wrappers over the libfedagg C-ABI (include/fedagg.h).
+
+Each wrapper validates shapes / dtypes / devices / alignment on the host, then
+launches on the current torch HIP stream.  None of them has a CPU fallback:
+they raise if the tensors are not fp32 HIP tensors or if libfedagg is absent.
+
+Reference arithmetic each op reproduces bit for bit:
+  reduce      SerialAggregator.add   fedsim/utils/aggregators.py:17-40
+              (+ FINALIZE: get/pop   fedsim/utils/aggregators.py:56-60,118-122)
+  finalize    SerialAggregator.pop   fedsim/utils/aggregators.py:118-122
+  fedavg_sgd  FedAvg.optimize        fedsim/distributed/centralized/training/fedavg.py:199-203
+  adabest_sgd AdaBest.optimize       fedsim/distributed/centralized/training/adabest.py:178-188
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native
+from ._native import FEDAGG_FINALIZE, FEDAGG_INIT, FEDAGG_NT, FEDAGG_SCALAR, check
+
+__all__ = [
+    "fl32",
+    "reduce_slab",
+    "reduce_rows",
+    "finalize",
+    "fedavg_sgd",
+    "adabest_sgd",
+    "tuning_flags",
+]
+
+
+def fl32(x) -> float:
+    """Round a Python int/float to the nearest fp32, as ATen does when a Python
+    scalar meets an fp32 tensor (``value * weight``, ``v / w``)."""
+    return float(np.float32(x))
+
+
+def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False) -> int:
+    sel = {0: 0, 4: 1, 8: 2, 16: 3}[unroll]
+    return (sel << _native.FEDAGG_UNROLL_SHIFT) | (vpt << _native.FEDAGG_VPT_SHIFT) | (
+        FEDAGG_NT if nt else 0
+    )
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_hip_f32(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must live on a HIP device, got {t.device}")
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def reduce_slab(
+    X: torch.Tensor,
+    w32: torch.Tensor,
+    out: torch.Tensor,
+    acc_in: Optional[torch.Tensor] = None,
+    W: Optional[float] = None,
+    P: Optional[int] = None,
+    flags: int = 0,
+) -> torch.Tensor:
+    """Weighted sequential reduction of the rows of ``X`` ([B, ldx] fp32, rows
+    contiguous) into ``out`` ([P]).  ``acc_in=None`` starts from +0.0; ``W`` not
+    None divides by fl32(W) on the way out (SerialAggregator.pop)."""
+    _require_hip_f32(X, "X")
+    _require_hip_f32(w32, "w32")
+    _require_hip_f32(out, "out")
+    if X.dim() != 2 or X.stride(1) != 1:
+        raise ValueError("X must be 2-D with contiguous rows")
+    B, ldx = X.shape[0], X.stride(0) if X.shape[0] > 1 else X.shape[1]
+    if P is None:
+        P = X.shape[1]
+    if P > X.shape[1]:
+        raise ValueError("P exceeds the row length of X")
+    if w32.numel() < B or not w32.is_contiguous():
+        raise ValueError("w32 must be contiguous with at least B entries")
+    if out.numel() < P or not out.is_contiguous():
+        raise ValueError("out must be contiguous with at least P entries")
+    f = flags
+    if acc_in is None:
+        f |= FEDAGG_INIT
+    else:
+        _require_hip_f32(acc_in, "acc_in")
+        if acc_in.numel() < P or not acc_in.is_contiguous():
+            raise ValueError("acc_in must be contiguous with at least P entries")
+    W32 = 0.0
+    if W is not None:
+        f |= FEDAGG_FINALIZE
+        W32 = fl32(W)
+    lib = _native.load()
+    rc = lib.fedagg_reduce_f32(
+        X.data_ptr(), ldx, w32.data_ptr(), B, P, _ptr(acc_in), out.data_ptr(),
+        W32, f, _stream_ptr(out.device),
+    )
+    check(rc, "fedagg_reduce_f32")
+    return out
+
+
+def reduce_rows(
+    rows: Sequence[torch.Tensor],
+    w32: torch.Tensor,
+    out: torch.Tensor,
+    acc_in: Optional[torch.Tensor] = None,
+    W: Optional[float] = None,
+    flags: int = 0,
+    table: Optional[torch.Tensor] = None,
+) -> torch.Tensor:
+    """Same as :func:`reduce_slab` but each client row is its own HIP tensor
+    (no packing copy).  ``table`` may pass a pre-filled int64 device tensor of
+    row pointers; otherwise one is built and uploaded."""
+    _require_hip_f32(out, "out")
+    _require_hip_f32(w32, "w32")
+    P = out.numel()
+    B = len(rows)
+    aligned = True
+    for i, r in enumerate(rows):
+        _require_hip_f32(r, f"rows[{i}]")
+        if r.numel() != P or not r.is_contiguous():
+            raise ValueError(f"rows[{i}] must be contiguous with {P} elements")
+        if r.data_ptr() % 16:
+            aligned = False
+    if table is None:
+        host = torch.tensor([r.data_ptr() for r in rows] or [0], dtype=torch.int64)
+        table = host.to(out.device, non_blocking=False)
+    f = flags
+    if acc_in is None:
+        f |= FEDAGG_INIT
+    else:
+        _require_hip_f32(acc_in, "acc_in")
+    W32 = 0.0
+    if W is not None:
+        f |= FEDAGG_FINALIZE
+        W32 = fl32(W)
+    lib = _native.load()
+    if not aligned:
+        f |= FEDAGG_SCALAR  # some row is not 16-B aligned: 4-byte-per-lane path
+    rc = lib.fedagg_reduce_rows_f32(
+        table.data_ptr(), w32.data_ptr(), B, P, _ptr(acc_in), out.data_ptr(), W32, f,
+        _stream_ptr(out.device),
+    )
+    check(rc, "fedagg_reduce_rows_f32")
+    return out
+
+
+def finalize(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = fl32(acc / fl32(W)) — SerialAggregator.pop's true division."""
+    _require_hip_f32(acc, "acc")
+    if out is None:
+        out = torch.empty_like(acc)
+    _require_hip_f32(out, "out")
+    rc = _native.load().fedagg_finalize_f32(
+        acc.data_ptr(), fl32(W), acc.numel(), out.data_ptr(), _stream_ptr(acc.device)
+    )
+    check(rc, "fedagg_finalize_f32")
+    return out
+
+
+def fedavg_sgd(avg: torch.Tensor, cloud: torch.Tensor, lr: float,
+               grad_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """In-place FedAvg server step with plain SGD on ``cloud``."""
+    _require_hip_f32(avg, "avg")
+    _require_hip_f32(cloud, "cloud")
+    if avg.numel() != cloud.numel():
+        raise ValueError("avg / cloud size mismatch")
+    if grad_out is not None:
+        _require_hip_f32(grad_out, "grad_out")
+    rc = _native.load().fedagg_fedavg_sgd_f32(
+        avg.data_ptr(), fl32(lr), cloud.data_ptr(), _ptr(grad_out), cloud.numel(),
+        _stream_ptr(cloud.device),
+    )
+    check(rc, "fedagg_fedavg_sgd_f32")
+    return cloud
+
+
+def adabest_sgd(avg: torch.Tensor, cloud: torch.Tensor, avg_prev: torch.Tensor,
+                beta: float, lr: float,
+                grad_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """In-place AdaBest server step (plain SGD) on ``cloud``; ``avg_prev`` <- avg."""
+    for t, n in ((avg, "avg"), (cloud, "cloud"), (avg_prev, "avg_prev")):
+        _require_hip_f32(t, n)
+        if t.numel() != cloud.numel():
+            raise ValueError(f"{n} size mismatch")
+    if grad_out is not None:
+        _require_hip_f32(grad_out, "grad_out")
+    rc = _native.load().fedagg_adabest_sgd_f32(
+        avg.data_ptr(), fl32(beta), fl32(lr), cloud.data_ptr(), avg_prev.data_ptr(),
+        _ptr(grad_out), cloud.numel(), _stream_ptr(cloud.device),
+    )
+    check(rc, "fedagg_adabest_sgd_f32")
+    return cloud

@@ -1,0 +1,133 @@
+/*
+ * fedagg.h — C-ABI of the MI355X (gfx950) server-side aggregation library
+ * (libfedagg.so, built from fedsim_amd/csrc/fedagg_kernels.hip).
+ *
+ * This is the drop-in boundary for FedSim's server aggregation hot path.
+ * The reference has no native code: each entry point replaces a piece of
+ * PyTorch-CPU arithmetic that the reference runs in Python.
+ *
+ *   fedagg_reduce_f32 / fedagg_reduce_rows_f32
+ *       replaces SerialAggregator.add            fedsim/utils/aggregators.py:17-40
+ *       (value*weight then sum_v+new_v, once per client, called from
+ *        serial_aggregation fedsim/distributed/centralized/training/utils.py:45-46)
+ *       and, with FEDAGG_FINALIZE, SerialAggregator.get/pop's  v / w
+ *                                                  fedsim/utils/aggregators.py:56-60,118-122
+ *   fedagg_finalize_f32
+ *       replaces SerialAggregator.get/pop's v / w  fedsim/utils/aggregators.py:56-60,118-122
+ *   fedagg_fedavg_sgd_f32
+ *       replaces FedAvg.optimize's pseudo-grad + torch.optim.SGD.step
+ *                                                  fedsim/distributed/centralized/training/fedavg.py:199-203
+ *   fedagg_adabest_sgd_f32
+ *       replaces AdaBest.optimize's h / new_params / pseudo-grad + SGD.step
+ *       + avg_params write-back                    fedsim/distributed/centralized/training/adabest.py:178-188
+ *
+ * Bit-exactness contract (exact mode, the default): every output equals the
+ * reference CPU aggregation bit for bit, given the same arrival order:
+ *     acc_0 = +0.0f ;  acc_{k+1} = fl32(acc_k + fl32(x_k * w_k))      (no FMA)
+ *     avg   = fl32(acc_K / W)                                        (true division)
+ * where w_k = fl32(python weight) and W = fl32(python sum of raw weights).
+ *
+ * Conventions
+ *   - All pointers are device pointers (HBM) unless stated; all buffers are
+ *     owned by the caller; the library allocates nothing and keeps no state.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *     Every call is asynchronous and stream-ordered.
+ *   - Return value: 0 on success, a positive hipError_t code if a HIP call
+ *     failed, or a negative FEDAGG_E* code for a rejected argument.
+ *     Nothing throws across the ABI.
+ */
+#ifndef FEDAGG_H_
+#define FEDAGG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FEDAGG_ABI_VERSION 1
+
+/* flags for the reduce entry points */
+#define FEDAGG_INIT      0x1  /* ignore acc_in: start from +0.0f (first batch of a round) */
+#define FEDAGG_FINALIZE  0x2  /* store fl32(acc / W32) instead of the raw sum              */
+#define FEDAGG_NT        0x4  /* non-temporal (streaming) loads of the client rows         */
+#define FEDAGG_SCALAR    0x8  /* force the 4-byte-per-lane path (rows not 16-B aligned)    */
+/* bits 8..11: k-unroll selector, 0 = library default, 1 = 4, 2 = 8, 3 = 16 */
+#define FEDAGG_UNROLL_SHIFT 8
+#define FEDAGG_UNROLL_MASK  0xF00
+/* bits 12..13: float4 columns per thread, 0 = default, 1 = 1, 2 = 2 */
+#define FEDAGG_VPT_SHIFT 12
+#define FEDAGG_VPT_MASK  0x3000
+
+/* negative error codes */
+#define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
+#define FEDAGG_EALIGN   (-23) /* internal: misaligned pointer passed to an aligned-only path */
+
+/* Version of this ABI (FEDAGG_ABI_VERSION). */
+int fedagg_abi_version(void);
+
+/* Human-readable message for a return code (static storage, never NULL). */
+const char* fedagg_strerror(int code);
+
+/*
+ * Weighted sequential reduction of B client rows into one accumulator.
+ *
+ *   X       row-major [B, ldx] fp32 slab; row k holds client k's flat params
+ *           (layout of vectorize_module, fedsim/utils/convert_parameters.py:78-94).
+ *           A parameter shard is addressed as X + offset with the same ldx.
+ *   ldx     row pitch in elements (>= P)
+ *   w       [B] fp32 per-client weights, already rounded to fp32
+ *   B, P    number of rows (B >= 0) and columns (P >= 0)
+ *   acc_in  [P] running sum from earlier batches (ignored with FEDAGG_INIT)
+ *   out     [P] destination; may alias acc_in
+ *   W32     fp32 total weight, used only with FEDAGG_FINALIZE
+ *
+ * For every column p, rows are consumed in order k = 0..B-1, so chaining
+ * batches through acc_in/out keeps the reference's arrival order.
+ * B == 0 with FEDAGG_INIT writes zeros (or 0/W32 when finalizing).
+ */
+int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B,
+                      int64_t P, const float* acc_in, float* out, float W32,
+                      int flags, void* stream);
+
+/*
+ * Same reduction, but row k lives at rows[k] (a device array of B device
+ * pointers, each to P contiguous fp32).  Lets the caller reduce client tensors
+ * already resident in HBM without packing them into a slab first.
+ * The table lives in device memory and is not inspected on the host: the
+ * caller must pass FEDAGG_SCALAR unless every rows[k] is 16-byte aligned.
+ */
+int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B,
+                           int64_t P, const float* acc_in, float* out, float W32,
+                           int flags, void* stream);
+
+/* out[p] = fl32(acc[p] / W32)  (IEEE true division; out may alias acc). */
+int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out,
+                        void* stream);
+
+/*
+ * FedAvg server step with plain SGD (no momentum / weight decay / nesterov):
+ *   g        = fl32(cloud - avg)
+ *   cloud'   = fma(-lr32, g, cloud)         (torch CPU SGD.step's add_(alpha=-lr))
+ * If grad_out != NULL the pseudo-gradient g is stored there too.
+ */
+int fedagg_fedavg_sgd_f32(const float* avg, float lr, float* cloud,
+                          float* grad_out, int64_t P, void* stream);
+
+/*
+ * AdaBest server step with plain SGD:
+ *   h        = fl32(beta32 * fl32(avg_prev - avg))
+ *   new      = fl32(avg - h)
+ *   g        = fl32(cloud - new)
+ *   cloud'   = fma(-lr32, g, cloud)
+ *   avg_prev'= avg
+ */
+int fedagg_adabest_sgd_f32(const float* avg, float beta, float lr, float* cloud,
+                           float* avg_prev, float* grad_out, int64_t P,
+                           void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAGG_H_ */

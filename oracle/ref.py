@@ -1,0 +1,125 @@
+"""ctypes binding of the C oracle (fedagg_ref.c) plus a numpy twin.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Host-side semantics the oracle also restates (pure Python, as the reference):
+  * weight of a client: ``train_weight`` or ``num_samples[train]``
+    (fedsim/distributed/centralized/training/utils.py:42-43); clients with
+    weight <= 0 are skipped (utils.py:45); a diverged client aborts (utils.py:39-40)
+  * total weight W: the Python running sum ``cur_w + new_w``
+    (fedsim/utils/aggregators.py:40) — int for FedAvg, float for FedNova
+  * rounding of a Python scalar against an fp32 tensor: fl32(scalar)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfedagg_ref.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
+        os.path.join(_HERE, "fedagg_ref.c")
+    ):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i64, f32, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, ctypes.c_int
+        L.ref_reduce_f32.argtypes = [vp, i64, vp, i64, i64, vp, vp, f32, ci]
+        L.ref_finalize_f32.argtypes = [vp, f32, i64, vp]
+        L.ref_fedavg_sgd_f32.argtypes = [vp, f32, vp, vp, i64]
+        L.ref_adabest_sgd_f32.argtypes = [vp, f32, f32, vp, vp, vp, i64]
+        for fn in ("ref_reduce_f32", "ref_finalize_f32", "ref_fedavg_sgd_f32",
+                   "ref_adabest_sgd_f32"):
+            getattr(L, fn).restype = None
+        _lib = L
+    return _lib
+
+
+def fl32(x) -> np.float32:
+    return np.float32(x)
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+def accepted(weights: Sequence, diverged: Optional[Sequence[bool]] = None):
+    """Indices and weights the reference adds, plus the round status.
+
+    Returns (idx, w, W, ok): ok is False if a diverged client aborted the round
+    (centralized_fl_algorithm.py:427-432); W is the Python running sum or None
+    when no client had weight > 0 (then "local_params" is not in the aggregator).
+    """
+    idx, ws, W = [], [], 0
+    for k, w in enumerate(weights):
+        if diverged is not None and diverged[k]:
+            return idx, ws, (W if idx else None), False
+        if w > 0:
+            idx.append(k)
+            ws.append(w)
+            W = W + w
+    return idx, ws, (W if idx else None), True
+
+
+def reduce(X: np.ndarray, weights: Sequence, acc_in: Optional[np.ndarray] = None,
+           W=None) -> np.ndarray:
+    """C oracle: weighted sequential reduce of rows of X ([B, P] fp32)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    B, P = X.shape
+    w32 = np.array([fl32(w) for w in weights], dtype=np.float32)
+    out = np.empty(P, dtype=np.float32)
+    lib().ref_reduce_f32(_p(X), P, _p(w32), B, P, _p(acc_in), _p(out),
+                         float(fl32(W)) if W is not None else 0.0, 1 if W is not None else 0)
+    return out
+
+
+def finalize(acc: np.ndarray, W) -> np.ndarray:
+    acc = np.ascontiguousarray(acc, dtype=np.float32)
+    out = np.empty_like(acc)
+    lib().ref_finalize_f32(_p(acc), float(fl32(W)), acc.size, _p(out))
+    return out
+
+
+def fedavg_sgd(avg: np.ndarray, cloud: np.ndarray, lr: float) -> np.ndarray:
+    c = np.array(cloud, dtype=np.float32, copy=True)
+    a = np.ascontiguousarray(avg, dtype=np.float32)
+    lib().ref_fedavg_sgd_f32(_p(a), float(fl32(lr)), _p(c), None, c.size)
+    return c
+
+
+def adabest_sgd(avg: np.ndarray, cloud: np.ndarray, avg_prev: np.ndarray, beta: float,
+                lr: float):
+    c = np.array(cloud, dtype=np.float32, copy=True)
+    ap = np.array(avg_prev, dtype=np.float32, copy=True)
+    a = np.ascontiguousarray(avg, dtype=np.float32)
+    lib().ref_adabest_sgd_f32(_p(a), float(fl32(beta)), float(fl32(lr)), _p(c), _p(ap), None,
+                              c.size)
+    return c, ap
+
+
+# ---- numpy twin (independent restatement of the reduce / divide) ----------
+
+def reduce_numpy(X: np.ndarray, weights: Sequence) -> np.ndarray:
+    acc = np.zeros(X.shape[1], dtype=np.float32)
+    for k in range(X.shape[0]):
+        prod = X[k].astype(np.float32) * np.float32(weights[k])
+        acc = acc + prod
+    return acc
+
+
+def finalize_numpy(acc: np.ndarray, W) -> np.ndarray:
+    return (acc / np.float32(W)).astype(np.float32)

@@ -1,0 +1,76 @@
+"""Pin the oracle: every oracle function must reproduce the reference's own
+outputs (tests/golden, produced by tools/gen_golden.py importing the reference)
+bit for bit.  CPU only."""
+import numpy as np
+import pytest
+
+from conftest import bits, golden_cases
+from oracle import ref
+from oracle import vectors as V
+
+CASES = golden_cases()
+PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"]]
+
+
+def _inputs(case):
+    X = V.client_rows(case["dist"], case["K"], case["P"], case["seed"])
+    assert V.sha256(X) == case["input_sha256"], "input generator drifted"
+    return X
+
+
+def _check(case, arrays, name, got):
+    assert V.sha256(got) == case["outputs_sha256"][name], name
+    if case["stored"]:
+        np.testing.assert_array_equal(bits(got), bits(arrays[f"{case['id']}/{name}"]))
+
+
+@pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
+def test_oracle_reduce_matches_reference(case, golden):
+    _, arrays = golden
+    X = _inputs(case)
+    idx, ws, W, ok = ref.accepted(case["weights"])
+    assert ok and W is not None
+    assert (W == case["scalars"]["W"]) and (isinstance(W, int) == case["scalars"]["W_is_int"])
+    s = ref.reduce(X[idx], ws)
+    _check(case, arrays, "sum", s)
+    _check(case, arrays, "avg", ref.reduce(X[idx], ws, W=W))
+    _check(case, arrays, "avg", ref.finalize(s, W))
+    if case["P"] <= 5000:
+        np.testing.assert_array_equal(bits(ref.reduce_numpy(X[idx], ws)), bits(s))
+        np.testing.assert_array_equal(bits(ref.finalize_numpy(s, W)), bits(ref.finalize(s, W)))
+
+
+@pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
+def test_oracle_optimize_matches_reference(case, golden):
+    _, arrays = golden
+    X = _inputs(case)
+    idx, ws, W, _ = ref.accepted(case["weights"])
+    avg = ref.reduce(X[idx], ws, W=W)
+    cloud0 = V.cloud_vector(case["P"], case["seed"] + 1)
+    for lr in case["lrs"]:
+        if case["algo"] == "adabest":
+            prev0 = V.cloud_vector(case["P"], case["seed"] + 2)
+            c, ap = ref.adabest_sgd(avg, cloud0, prev0, case["beta"], lr)
+            _check(case, arrays, f"avg_params_lr{lr}", ap)
+        else:
+            c = ref.fedavg_sgd(avg, cloud0, lr)
+        _check(case, arrays, f"cloud_lr{lr}", c)
+
+
+def test_oracle_edge_cases():
+    by_id = {c["id"]: c for c in CASES}
+    zero = [c for c in CASES if c.get("zero_at")]
+    assert zero, "golden set lost its zero-weight cases"
+    for c in zero:
+        idx, ws, W, ok = ref.accepted(c["weights"])
+        assert ok
+        assert c["has_params"] == (W is not None)
+        if W is None:
+            assert c["reports"] == {}
+    div = [c for c in CASES if c.get("diverged_at") is not None]
+    assert div
+    for c in div:
+        diverged = [k == c["diverged_at"] for k in range(c["K"])]
+        _, _, _, ok = ref.accepted(c["weights"], diverged)
+        assert not ok and c["ok"][-1] is False and len(c["ok"]) == c["diverged_at"] + 1
+    assert by_id
