@@ -198,13 +198,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(Rows rows,
   const int64_t block_end = static_cast<int64_t>(blockIdx.x + 1) * (kBlock * VPT);
   if (block_end <= nvec) {
     reduce_vec_body<U, VPT, NT, false>(rows, w, B, nvec, acc_in, out, W32, flags);
-  } else {
-    if (nvec > 0)
-      reduce_vec_body<U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
-    // The last block also owns the (P % 4) scalar tail columns.
-    if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
-      reduce_scalar_cols<NT>(rows, w, B, nvec * 4 + threadIdx.x, acc_in, out, W32, flags);
+  } else if (nvec > 0) {
+    reduce_vec_body<U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
   }
+  // The last block also owns the (P % 4) scalar tail columns.
+  if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
+    reduce_scalar_cols<NT>(rows, w, B, nvec * 4 + threadIdx.x, acc_in, out, W32, flags);
 }
 
 // Generic path for rows that are not 16-byte aligned: one column per lane,

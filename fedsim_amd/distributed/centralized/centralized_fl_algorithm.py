@@ -1,0 +1,330 @@
+"""CentralFLAlgorithm — the round driver and the static user-method plugin contract.
+
+Same constructor, storage entries, user-method table and round loop as the
+reference (fedsim/distributed/centralized/centralized_fl_algorithm.py:30-828).
+The one change on the hot path: the per-round aggregator created at :417 is
+the device-backed ``fedsim_amd.utils.SerialAggregator``, so every
+``receive_from_client`` streams its client vector into HBM and ``optimize``
+pops a kernel-reduced average.  ``aggregator_factory`` lets a caller pass slab
+/ device / tuning options for that aggregator.
+"""
+from __future__ import annotations
+
+import inspect
+import random
+from functools import partial
+from typing import Any, Dict, Optional
+
+import torch
+from torch import nn
+from torch.utils.data import DataLoader
+
+from ... import scores as _scores
+from ...utils import AppendixAggregator, SerialAggregator, Storage, apply_on_dict
+
+try:  # progress bar is cosmetic
+    from tqdm import trange as _trange
+except Exception:  # pragma: no cover
+    _trange = range
+
+
+class CentralFLAlgorithm(object):
+    def __init__(
+        self,
+        data_manager,
+        metric_logger,
+        num_clients,
+        sample_scheme,
+        sample_rate,
+        model_def,
+        epochs,
+        criterion_def,
+        optimizer_def=partial(torch.optim.SGD, lr=1.0),
+        local_optimizer_def=partial(torch.optim.SGD, lr=0.1),
+        lr_scheduler_def=None,
+        local_lr_scheduler_def=None,
+        r2r_local_lr_scheduler_def=None,
+        batch_size=32,
+        test_batch_size=64,
+        device="cpu",
+        *args,
+        aggregator_factory=None,
+        progress=False,
+        **kwargs,
+    ):
+        sample_count = int(sample_rate * num_clients)
+        if not 1 <= sample_count <= num_clients:
+            raise Exception(
+                "invalid client sample size for {}% of {} clients".format(sample_rate, num_clients)
+            )
+        model_def_ = getattr(model_def, "func", model_def)
+        if not (inspect.isclass(model_def_) and issubclass(model_def_, nn.Module)) and not callable(
+            model_def
+        ):
+            raise Exception("incompatiple model!")
+        if isinstance(criterion_def, str) and hasattr(_scores, criterion_def):
+            criterion_def = getattr(_scores, criterion_def)
+
+        r2r_local_lr_scheduler = None
+        if r2r_local_lr_scheduler_def is not None:
+            if hasattr(local_optimizer_def, "keywords"):
+                clr = local_optimizer_def.keywords["lr"]
+            elif "lr" in inspect.signature(local_optimizer_def).parameters:
+                clr = inspect.signature(local_optimizer_def).parameters["lr"].default
+            else:
+                raise Exception("lr not found in local optimizer class")
+            dummy_opt = torch.optim.SGD(params=[torch.tensor([1.0, 1.0], requires_grad=True)],
+                                        lr=clr)
+            r2r_local_lr_scheduler = r2r_local_lr_scheduler_def(dummy_opt)
+            if not hasattr(r2r_local_lr_scheduler, "get_last_lr"):
+                sch = r2r_local_lr_scheduler
+                sch.get_last_lr = lambda: sch._last_lr
+            dummy_opt.step()
+
+        global_dataloaders = {
+            key: DataLoader(dataset, batch_size=test_batch_size, pin_memory=False)
+            for key, dataset in data_manager.get_global_dataset().items()
+        }
+        oracle_dataset = data_manager.get_oracle_dataset()
+
+        self._aggregator_factory = aggregator_factory or SerialAggregator
+        self._progress = progress
+        self._server_memory = Storage()
+        w = self._server_memory.write
+        for key, val in (("data_manager", data_manager), ("num_clients", num_clients),
+                         ("sample_count", sample_count), ("sample_scheme", sample_scheme),
+                         ("oracle_dataset", oracle_dataset), ("last_client_sampled", None)):
+            w(key, val, read_protected=True, write_protected=True)
+        for key, val in (("test_batch_size", test_batch_size), ("optimizer_def", optimizer_def),
+                         ("lr_scheduler_def", lr_scheduler_def),
+                         ("r2r_local_lr_scheduler", r2r_local_lr_scheduler),
+                         ("criterion_def", criterion_def), ("model_def", model_def),
+                         ("metric_logger", metric_logger), ("device", device),
+                         ("global_dataloaders", global_dataloaders), ("rounds", 0)):
+            w(key, val, write_protected=True)
+
+        self._client_memory = {k: Storage() for k in range(num_clients)}
+        self._local_cfg = Storage()
+        for key, val in (("epochs", epochs), ("batch_size", batch_size),
+                         ("test_batch_size", test_batch_size), ("criterion_def", criterion_def),
+                         ("local_optimizer_def", local_optimizer_def),
+                         ("local_lr_scheduler_def", local_lr_scheduler_def)):
+            self._local_cfg.write(key, val, write_protected=True)
+        self._local_cfg.write("device", device)
+        self._train_split_name = "train"
+        self._server_scores = {key: dict() for key in global_dataloaders}
+        self._client_scores = {key: dict() for key in data_manager.get_local_splits_names()}
+
+        self.user_methods = dict(
+            init=self.__class__.init,
+            at_round_start=self.__class__.at_round_start,
+            at_round_end=self.__class__.at_round_end,
+            deploy=self.__class__.deploy,
+            optimize=self.__class__.optimize,
+            report=self.__class__.report,
+            receive_from_client=self.__class__.receive_from_client,
+            send_to_client=self.__class__.send_to_client,
+            send_to_server=self.__class__.send_to_server,
+        )
+        for key, value in self.user_methods.items():
+            if "self" in inspect.signature(value).parameters:
+                raise Exception(
+                    f"Remove `self` from {key} arguments. All user methods should be static!"
+                )
+        self.user_methods["init"](self._server_memory, *args, **kwargs)
+
+    # ---- round plumbing (centralized_fl_algorithm.py:299-443) -------------
+    def _sample_clients(self):
+        mem = self._server_memory
+        scheme = mem.read("sample_scheme", silent=True)
+        count = mem.read("sample_count", silent=True)
+        n = mem.read("num_clients", silent=True)
+        last = mem.read("last_client_sampled", silent=True)
+        if scheme == "uniform":
+            return random.sample(range(n), count)
+        if scheme == "sequential":
+            last = -1 if last is None else last
+            clients = [(i + 1) % n for i in range(last, last + count)]
+            mem.write("last_client_sampled", clients[-1], silent=True)
+            return clients
+        raise NotImplementedError
+
+    def _send_to_client(self, client_id):
+        return self.user_methods["send_to_client"](self._server_memory, client_id=client_id)
+
+    def _send_to_server(self, client_id):
+        r2r = self._server_memory.read("r2r_local_lr_scheduler")
+        data_manager = self._server_memory.read("data_manager", silent=True)
+        rounds = self._server_memory.read("rounds")
+        cfg = self._local_cfg
+        local_optimizer_def = cfg.read("local_optimizer_def")
+        if r2r is not None:
+            local_optimizer_def = partial(local_optimizer_def, lr=r2r.get_last_lr()[0])
+        client_ctx = self.user_methods["send_to_server"](
+            client_id, rounds, self._client_memory[client_id],
+            data_manager.get_local_dataset(client_id), self.get_train_split_name(),
+            self.get_local_scores(), cfg.read("epochs"), cfg.read("criterion_def")(),
+            cfg.read("batch_size"), cfg.read("test_batch_size"), local_optimizer_def,
+            cfg.read("local_lr_scheduler_def"), cfg.read("device"),
+            ctx=self._send_to_client(client_id),
+        )
+        if not isinstance(client_ctx, dict):
+            raise Exception("client should only return a dict!")
+        return {**client_ctx, "client_id": client_id}
+
+    def _receive_from_client(self, client_msg, serial_aggregator, appendix_aggregator):
+        client_id = client_msg.pop("client_id")
+        return self.user_methods["receive_from_client"](
+            self._server_memory, client_id, client_msg, self.get_train_split_name(),
+            serial_aggregator, appendix_aggregator,
+        )
+
+    def _optimize(self, serial_aggregator, appendix_aggregator):
+        return self.user_methods["optimize"](self._server_memory, serial_aggregator,
+                                             appendix_aggregator)
+
+    def _report(self, round_scores, optimize_reports=None, deployment_points=None):
+        mem = self._server_memory
+        metric_logger = mem.read("metric_logger")
+        rounds = mem.read("rounds")
+        report_metrics = self.user_methods["report"](
+            mem, mem.read("global_dataloaders", silent=True), rounds, round_scores,
+            metric_logger, mem.read("device"), optimize_reports, deployment_points,
+        )
+        if metric_logger is not None:
+            apply_on_dict(report_metrics, metric_logger.log_scalar, step=rounds)
+        return report_metrics
+
+    def _train(self, rounds, num_score_report_point=None):
+        diverged = False
+        cur_round = self._server_memory.read("rounds")
+        score_aggregator = AppendixAggregator(max_deque_lenght=num_score_report_point)
+        loop = _trange(rounds + 1) if self._progress else range(rounds + 1)
+        for round_num in loop:
+            self._at_round_start()
+            round_serial_aggregator = self._aggregator_factory()
+            round_appendix_aggregator = AppendixAggregator()
+            for client_id in self._sample_clients():
+                client_msg = self._send_to_server(client_id)
+                success = self._receive_from_client(client_msg, round_serial_aggregator,
+                                                    round_appendix_aggregator)
+                if not success:
+                    diverged = True
+                    break
+            if diverged:
+                # drop the round's slab without launching
+                del round_serial_aggregator
+                return score_aggregator.pop_all()
+            opt_reports = self._optimize(round_serial_aggregator, round_appendix_aggregator)
+            deploy_point = self.user_methods["deploy"](self._server_memory)
+            score_dict = self._report(self.get_global_scores(), opt_reports, deploy_point)
+            score_aggregator.append_all(score_dict, step=cur_round)
+            self._at_round_end(score_aggregator)
+            self._server_memory.write("rounds", cur_round + round_num + 1, silent=True)
+        return score_aggregator.pop_all()
+
+    def _at_round_start(self) -> None:
+        self.user_methods["at_round_start"](self._server_memory)
+
+    def _at_round_end(self, score_aggregator) -> None:
+        r2r = self._server_memory.read("r2r_local_lr_scheduler")
+        if r2r is not None:
+            r2r.step()
+        self.user_methods["at_round_end"](self._server_memory, score_aggregator)
+
+    def _get_round_scores(self, score_def_deck):
+        rounds = self._server_memory.read("rounds")
+        out = dict()
+        for name, definition in score_def_deck.items():
+            obj = definition()
+            if rounds % obj.log_freq == 0:
+                out[name] = obj
+        return out
+
+    # ---- public API (centralized_fl_algorithm.py:466-631) -----------------
+    def train(self, rounds: int, num_score_report_point: Optional[int] = None,
+              train_split_name="train") -> Optional[Dict[str, Optional[float]]]:
+        default_split_name = self._train_split_name
+        self._train_split_name = train_split_name
+        ans = self._train(rounds=rounds, num_score_report_point=num_score_report_point)
+        self._train_split_name = default_split_name
+        return ans
+
+    def get_model_def(self):
+        return self._server_memory.read("model_def")
+
+    def get_server_storage(self):
+        return self._server_memory
+
+    def get_round_number(self):
+        return self._server_memory.read("rounds")
+
+    def get_train_split_name(self):
+        return self._train_split_name
+
+    def get_global_loader_split(self, split_name):
+        return self._server_memory.read("global_dataloaders")[split_name]
+
+    def get_device(self) -> str:
+        return self._server_memory.read("device")
+
+    def hook_local_score(self, score_def, score_name, split_name) -> None:
+        self._client_scores[split_name][score_name] = score_def
+
+    def hook_global_score(self, score_def, score_name, split_name) -> None:
+        self._server_scores[split_name][score_name] = score_def
+
+    def get_local_split_scores(self, split_name) -> Dict[str, Any]:
+        return self._get_round_scores(self._client_scores[split_name])
+
+    def get_global_split_scores(self, split_name):
+        split_scores = self._get_round_scores(self._server_scores[split_name])
+        return split_scores if len(split_scores) > 0 else None
+
+    def get_local_scores(self) -> Dict[str, Any]:
+        out = dict()
+        for split_name in self._client_scores:
+            s = self.get_local_split_scores(split_name)
+            if s is not None:
+                out[split_name] = s
+        return out
+
+    def get_global_scores(self) -> Dict[str, Any]:
+        out = dict()
+        for split_name in self._server_scores:
+            s = self.get_global_split_scores(split_name)
+            if s is not None:
+                out[split_name] = s
+        return out
+
+    # ---- user methods (static; centralized_fl_algorithm.py:636-828) -------
+    def init(server_storage, *args, **kwargs) -> None:
+        pass
+
+    def at_round_start(server_storage) -> None:
+        pass
+
+    def at_round_end(server_storage, score_aggregator) -> None:
+        pass
+
+    def send_to_client(server_storage, client_id):
+        raise NotImplementedError("Algorithm is missing the required 'send_to_client' function")
+
+    def send_to_server(id, rounds, storage, datasets, train_split_name, scores, epochs,
+                       criterion, train_batch_size, inference_batch_size, optimizer_def,
+                       lr_scheduler_def=None, device="cuda", ctx=None, *args, **kwargs):
+        raise NotImplementedError("Algorithm is missing the required 'send_to_server' function")
+
+    def receive_from_client(server_storage, client_id, client_msg, train_split_name,
+                            serial_aggregator, appendix_aggregator) -> bool:
+        raise NotImplementedError
+
+    def optimize(server_storage, serial_aggregator, appendix_aggregator):
+        raise NotImplementedError
+
+    def deploy(server_storage):
+        raise NotImplementedError
+
+    def report(server_storage, dataloaders, round_scores, metric_logger, device,
+               optimize_reports, deployment_points=None):
+        raise NotImplementedError

@@ -1,0 +1,55 @@
+"""Flat-vector <-> module parameter conversion (the pack / unpack edges of the
+path).  Layout = concatenation of ``module.parameters()`` in registration order,
+each parameter's row-major storage (reference: fedsim/utils/convert_parameters.py:78-94,
+129-148)."""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+from torch import Tensor
+from torch.nn import Module
+from torch.nn.utils import parameters_to_vector, vector_to_parameters
+
+
+def vector_to_parameters_like(vec: Tensor, parameters_like):
+    """Views of ``vec`` shaped like each of ``parameters_like`` (no copy)."""
+    if not isinstance(vec, torch.Tensor):
+        raise TypeError("expected torch.Tensor, but got: {}".format(torch.typename(vec)))
+    out, ptr = [], 0
+    for p in parameters_like:
+        n = p.numel()
+        out.append(vec[ptr: ptr + n].view_as(p).data)
+        ptr += n
+    return out
+
+
+def vector_to_named_parameters_like(vec: Tensor, named_parameters_like) -> OrderedDict:
+    if not isinstance(vec, torch.Tensor):
+        raise TypeError("expected torch.Tensor, but got: {}".format(torch.typename(vec)))
+    out, ptr = OrderedDict(), 0
+    for key, p in named_parameters_like:
+        n = p.numel()
+        out[key] = vec[ptr: ptr + n].view_as(p)
+        ptr += n
+    return out
+
+
+def vectorize_module(module: Module, clone=True, detach=True) -> Tensor:
+    vec = parameters_to_vector(module.parameters())
+    if clone:
+        vec = vec.clone()
+    if detach:
+        vec = vec.detach()
+    return vec
+
+
+def initialize_module(module: Module, vec: Tensor, clone=True, detach=True) -> bool:
+    if clone:
+        vec = vec.clone()
+    if detach:
+        vec = vec.detach()
+    if sum(p.numel() for p in module.parameters()) != vec.numel():
+        return False
+    vector_to_parameters(vec, module.parameters())
+    return True

@@ -98,6 +98,33 @@ def client_weights(kind: str, K: int, seed: int):
     raise ValueError(kind)
 
 
+def client_messages(X: np.ndarray, weights, diverged_at=None, device=None):
+    """Client messages shaped like FedAvg.send_to_server's return
+    (fedsim/distributed/centralized/training/fedavg.py:173-179).  The train
+    split's sample count carries the weight; per-split scalar metrics exercise
+    serial_aggregation's metric path (training/utils.py:47-51)."""
+    import torch
+
+    msgs = []
+    for k in range(X.shape[0]):
+        w = weights[k]
+        n = w if isinstance(w, int) else int(round(w * 10))
+        params = torch.from_numpy(X[k].copy())
+        if device is not None:
+            params = params.to(device)
+        msgs.append(
+            dict(
+                local_params=params,
+                num_steps=max(1, n // 32),
+                diverged=(diverged_at is not None and k == diverged_at),
+                num_samples={"train": n, "test": 100 + k},
+                metrics={"train": {"loss": 2.0 + 0.01 * k, "acc": 0.1 * (k % 7)},
+                         "test": {"acc": 0.05 * (k % 5)}},
+            )
+        )
+    return msgs
+
+
 def cloud_vector(P: int, seed: int) -> np.ndarray:
     return (0.05 * gauss(seed * 7919 + 7, P) + 1e-2 * gauss(seed * 5 + 99991, P)).astype(
         np.float32

@@ -1,0 +1,120 @@
+"""CPU-side checks of the C-ABI boundary: libfedagg.so loads into torch's HIP
+runtime, exports every entry point include/fedagg.h declares, its constants
+match the Python mirror, and argument validation rejects bad calls before any
+device work (no GPU needed for any of this)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "fedagg.h")
+LIB = os.path.join(REPO, "fedsim_amd", "libfedagg.so")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(fedagg_[a-z0-9_]+)\s*\(", text)))
+
+
+def header_defines():
+    out = {}
+    for m in re.finditer(r"#define\s+(FEDAGG_[A-Z_]+)\s+\(?(-?0x[0-9A-Fa-f]+|-?\d+)\)?",
+                         open(HEADER).read()):
+        out[m.group(1)] = int(m.group(2), 0)
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import torch  # noqa: F401
+    from fedsim_amd import _native
+
+    return _native.load()
+
+
+def test_header_declares_the_abi():
+    fns = header_functions()
+    assert fns == sorted([
+        "fedagg_abi_version", "fedagg_strerror", "fedagg_reduce_f32", "fedagg_reduce_rows_f32",
+        "fedagg_finalize_f32", "fedagg_fedavg_sgd_f32", "fedagg_adabest_sgd_f32",
+    ])
+
+
+def test_library_exports_every_declared_symbol(lib):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for fn in header_functions():
+        assert fn in exported, fn
+        assert hasattr(lib, fn)
+
+
+def test_python_mirror_matches_header(lib):
+    from fedsim_amd import _native
+
+    d = header_defines()
+    assert _native.ABI_VERSION == d["FEDAGG_ABI_VERSION"] == lib.fedagg_abi_version()
+    for name in ("FEDAGG_INIT", "FEDAGG_FINALIZE", "FEDAGG_NT", "FEDAGG_SCALAR",
+                 "FEDAGG_UNROLL_SHIFT", "FEDAGG_VPT_SHIFT", "FEDAGG_EINVAL"):
+        assert getattr(_native, name) == d[name], name
+    assert set(_native.exported_symbols()) == set(header_functions())
+
+
+def test_single_hip_runtime(lib):
+    from fedsim_amd import _native
+
+    assert len(_native._hip_runtimes_mapped()) == 1
+
+
+def test_argument_validation_without_device(lib):
+    E = -22
+    null = None
+    # negative sizes
+    assert lib.fedagg_reduce_f32(null, 0, null, -1, 4, null, null, 1.0, 1, null) == E
+    assert lib.fedagg_reduce_f32(null, 0, null, 1, -4, null, null, 1.0, 1, null) == E
+    # missing output / weights / rows / accumulator
+    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, null, 1.0, 1, null) == E
+    assert lib.fedagg_reduce_f32(16, 4, null, 1, 4, null, 16, 1.0, 1, null) == E
+    assert lib.fedagg_reduce_f32(null, 4, 16, 1, 4, null, 16, 1.0, 1, null) == E
+    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 0, null) == E  # no INIT, no acc
+    assert lib.fedagg_reduce_f32(16, 2, 16, 1, 4, null, 16, 1.0, 1, null) == E  # ldx < P
+    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 1 | 0x10000, null) == E
+    assert lib.fedagg_reduce_f32(16, 1 << 31, 16, 1, (1 << 30) + 1, null, 16, 1.0, 1, null) == E
+    assert lib.fedagg_reduce_rows_f32(null, 16, 1, 4, null, 16, 1.0, 1, null) == E
+    assert lib.fedagg_finalize_f32(null, 1.0, 4, 16, null) == E
+    assert lib.fedagg_finalize_f32(16, 1.0, -1, 16, null) == E
+    assert lib.fedagg_fedavg_sgd_f32(16, 1.0, 17, null, 4, null) == E  # misaligned
+    assert lib.fedagg_adabest_sgd_f32(16, 0.6, 1.0, 16, null, null, 4, null) == E
+    # P == 0 is a no-op success
+    assert lib.fedagg_reduce_f32(null, 0, null, 0, 0, null, null, 1.0, 1, null) == 0
+    assert lib.fedagg_finalize_f32(null, 1.0, 0, null, null) == 0
+    assert lib.fedagg_strerror(E) == b"fedagg: invalid argument"
+    assert lib.fedagg_strerror(0) == b"success"
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+
+    from fedsim_amd import ops
+
+    with pytest.raises(ValueError, match="HIP device"):
+        ops.reduce_slab(torch.ones(2, 3), torch.ones(2), torch.empty(3))
+    with pytest.raises(TypeError, match="float32"):
+        ops.finalize(torch.ones(3, dtype=torch.float64), 2)
+
+
+def test_build_is_gfx950():
+    out = subprocess.check_output(
+        ["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
+         f"--input={LIB}"], text=True, stderr=subprocess.STDOUT,
+    ) if os.path.exists("/opt/rocm/lib/llvm/bin/clang-offload-bundler") else ""
+    if not out:
+        raw = open(LIB, "rb").read()
+        assert b"gfx950" in raw
+    else:
+        assert "gfx950" in out
+    assert ctypes.sizeof(ctypes.c_void_p) == 8

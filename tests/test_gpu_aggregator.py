@@ -1,0 +1,196 @@
+"""GPU parity through the plugin surface: FedAvg / AdaBest / FedNova
+receive_from_client + optimize on the device-backed SerialAggregator, against
+the reference's golden outputs (bit-exact), with client vectors arriving on the
+host (H2D path) or already in HBM (D2D path)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits, golden_cases
+from oracle import ref
+from oracle import vectors as V
+
+pytestmark = pytest.mark.gpu
+
+CASES = golden_cases()
+PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"]]
+FLOW_CASES = [c for c in PARAM_CASES if c["P"] <= 1_100_000]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+def _expect(case, arrays, name, got):
+    got = np.ascontiguousarray(got, dtype=np.float32)
+    assert V.sha256(got) == case["outputs_sha256"][name], f"{case['id']}:{name}"
+    if case["stored"]:
+        np.testing.assert_array_equal(bits(got), bits(arrays[f"{case['id']}/{name}"]))
+
+
+def _receive_all(algo_cls, case, agg, msgs, storage):
+    from fedsim_amd.distributed.centralized.training import serial_aggregation
+
+    for k, msg in enumerate(msgs):
+        if case["algo"] == "adabest":
+            ok = serial_aggregation(storage, k, msg, "train", agg, train_weight=1)
+        elif case["algo"] == "fednova":
+            ok = serial_aggregation(storage, k, msg, "train", agg,
+                                    train_weight=case["weights"][k])
+        else:
+            ok = algo_cls.receive_from_client(storage, k, msg, "train", agg, None)
+        assert ok
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("case", FLOW_CASES, ids=[c["id"] for c in FLOW_CASES])
+def test_algorithm_round_bitwise(case, where, dev, golden):
+    from fedsim_amd.distributed.centralized.training import AdaBest, FedAvg
+    from fedsim_amd.utils import SerialAggregator, Storage
+
+    _, arrays = golden
+    X = V.client_rows(case["dist"], case["K"], case["P"], case["seed"])
+    weights = list(case["weights"])
+    cloud0 = V.cloud_vector(case["P"], case["seed"] + 1)
+    cloud_dev = dev if where == "device" else torch.device("cpu")
+    for lr in case["lrs"]:
+        msgs = V.client_messages(X, weights, device=dev if where == "device" else None)
+        st = Storage()
+        agg = SerialAggregator(max_rows=5)  # force several slab flushes
+        _receive_all(FedAvg, case, agg, msgs, st)
+        # non-destructive reads first (get / get_sum / get_weight)
+        W = agg.get_weight("local_params")
+        assert W == case["scalars"]["W"]
+        s = agg.get_sum("local_params")
+        assert s.device.type == ("cuda" if where == "device" else "cpu")
+        _expect(case, arrays, "sum", s.cpu().numpy())
+        _expect(case, arrays, "avg", agg.get("local_params").cpu().numpy())
+        cloud = torch.from_numpy(cloud0.copy()).to(cloud_dev).requires_grad_(True)
+        st.write("cloud_params", cloud)
+        st.write("optimizer", torch.optim.SGD(params=[cloud], lr=lr))
+        st.write("lr_scheduler", None)
+        if case["algo"] == "adabest":
+            prev0 = V.cloud_vector(case["P"], case["seed"] + 2)
+            st.write("avg_params", torch.from_numpy(prev0.copy()).to(cloud_dev))
+            st.write("beta", case["beta"])
+            reports = AdaBest.optimize(st, agg, None)
+            ap = st.read("avg_params")
+            assert ap.device == cloud_dev
+            _expect(case, arrays, f"avg_params_lr{lr}", ap.cpu().numpy())
+        else:
+            reports = FedAvg.optimize(st, agg, None)
+        _expect(case, arrays, f"cloud_lr{lr}", cloud.detach().cpu().numpy())
+        assert "local_params" not in agg
+        assert reports.keys() == case["reports"].keys()
+        for k, v in case["reports"].items():
+            assert float(reports[k]) == v, k
+
+
+def test_zero_weight_and_diverged_rounds(dev, golden):
+    from fedsim_amd.distributed.centralized.training import FedAvg
+    from fedsim_amd.utils import SerialAggregator, Storage
+
+    for case in CASES:
+        if not (case.get("zero_at") or case.get("diverged_at") is not None):
+            continue
+        X = V.client_rows(case["dist"], case["K"], case["P"], case["seed"])
+        msgs = V.client_messages(X, case["weights"], case.get("diverged_at"))
+        agg, st, oks = SerialAggregator(), Storage(), []
+        for k, msg in enumerate(msgs):
+            oks.append(FedAvg.receive_from_client(st, k, msg, "train", agg, None))
+            if not oks[-1]:
+                break
+        assert oks == case["ok"]
+        assert ("local_params" in agg) == case["has_params"]
+        if all(oks) and not case["has_params"]:
+            assert {k: float(v) for k, v in agg.pop_all().items()} == case["reports"]
+
+
+def test_aggregator_semantics_on_device(dev):
+    from fedsim_amd.utils import SerialAggregator
+
+    agg = SerialAggregator(max_rows=2)
+    a = torch.randn(3, 5, 7)
+    b = torch.randn(3, 5, 7)
+    agg.add("t", a, 3)
+    first = agg.get("t")
+    assert first.shape == (3, 5, 7) and first.device.type == "cpu"
+    np.testing.assert_array_equal(bits(first.numpy()), bits((a * 3 / 3).numpy()))
+    agg.add("t", b, 5)
+    exp = (0 + a * 3 + b * 5) / 8
+    np.testing.assert_array_equal(bits(agg.pop("t").numpy()), bits(exp.numpy()))
+    with pytest.raises(Exception, match="is not in the aggregator"):
+        agg.pop("t")
+    with pytest.raises(TypeError):
+        agg.add("u", torch.ones(4), None)
+    with pytest.raises(TypeError):
+        agg.add("v", torch.ones(4, dtype=torch.float64), 1)
+    # weights summing to zero -> raw sum (aggregators.py:56-57)
+    agg.add("z", torch.ones(4), 2)
+    agg.add("z", torch.ones(4), -2)
+    assert agg.get_weight("z") == 0
+    assert torch.equal(agg.pop("z"), torch.zeros(4))
+    # zero-size tensor key
+    agg.add("e", torch.empty(0), 1)
+    assert agg.pop("e").numel() == 0
+    # device in, device out
+    d = torch.randn(1000, device=dev)
+    agg.add("d", d, 7)
+    r = agg.pop("d")
+    assert r.device == d.device
+    np.testing.assert_array_equal(bits(r.cpu().numpy()), bits(((0 + d.cpu() * 7) / 7).numpy()))
+
+
+def test_pinned_source_is_snapshotted(dev):
+    from fedsim_amd.utils import SerialAggregator
+
+    agg = SerialAggregator()
+    src = torch.ones(1 << 20).pin_memory()
+    agg.add("p", src, 1)
+    src.fill_(5.0)  # the aggregator must have copied the value at add time
+    agg.add("p", src, 1)
+    out = agg.pop("p")
+    assert torch.equal(out, torch.full((1 << 20,), 3.0))
+
+
+def test_full_size_properties(dev):
+    """Headline size (K=1000 x P=25M, 100 GB in HBM): size-independent
+    properties + bitwise oracle parity on sampled columns."""
+    from fedsim_amd import ops
+
+    K, P = 1000, 25_000_000
+    free, _ = torch.cuda.mem_get_info(dev)
+    if free < 120e9:
+        pytest.skip("needs >120 GB of free HBM")
+    ldx = (P + 63) // 64 * 64
+    X = torch.empty((K, ldx), device=dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    for k0 in range(0, K, 100):
+        X[k0:k0 + 100].normal_(0, 1, generator=g)
+    Xv = X[:, :P]
+    w = [int(v) for v in np.random.default_rng(11).integers(50, 601, size=K)]
+    W = sum(w)
+    w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
+    out = torch.empty(P, device=dev)
+    ops.reduce_slab(Xv, w32, out, W=W)
+    # (1) streamed in uneven batches through the accumulator == single pass
+    acc = torch.empty(P, device=dev)
+    bounds = [0, 1, 17, 300, 301, 777, K]
+    for i in range(len(bounds) - 1):
+        k0, k1 = bounds[i], bounds[i + 1]
+        ops.reduce_slab(Xv[k0:k1], w32[k0:k1].contiguous(), acc, acc_in=None if k0 == 0 else acc,
+                        W=W if k1 == K else None, P=P)
+    assert torch.equal(acc.view(torch.int32), out.view(torch.int32))
+    # (2) power-of-two weight scaling is exact: sum(2w) == 2 sum(w)
+    s1 = torch.empty(P, device=dev)
+    s2 = torch.empty(P, device=dev)
+    ops.reduce_slab(Xv, w32, s1)
+    ops.reduce_slab(Xv, (w32 * 2).contiguous(), s2)
+    assert torch.equal((s1 * 2).view(torch.int32), s2.view(torch.int32))
+    # (3) bitwise vs the oracle on 4096 sampled columns
+    cols = torch.from_numpy(np.random.default_rng(3).choice(P, size=4096, replace=False)).to(dev)
+    sub = Xv.index_select(1, cols).cpu().numpy()
+    exp = ref.reduce(sub, w, W=W)
+    np.testing.assert_array_equal(bits(out.index_select(0, cols).cpu().numpy()), bits(exp))

@@ -1,0 +1,137 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the reference's golden
+outputs and the pinned oracle.  Bar: bit-exact (exact mode)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits, golden_cases
+from oracle import ref
+from oracle import vectors as V
+
+pytestmark = pytest.mark.gpu
+
+CASES = golden_cases()
+PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"]]
+VARIANTS = {
+    "default": dict(),
+    "u4v2nt": dict(unroll=4, vpt=2, nt=True),
+    "u8v1": dict(unroll=8, vpt=1),
+    "u16v2": dict(unroll=16, vpt=2),
+    "u4v1nt": dict(unroll=4, vpt=1, nt=True),
+}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from fedsim_amd import _native
+
+    _native.load()
+    return torch.device("cuda:0")
+
+
+def _inputs(case):
+    X = V.client_rows(case["dist"], case["K"], case["P"], case["seed"])
+    assert V.sha256(X) == case["input_sha256"]
+    return X
+
+
+def _expect(case, arrays, name, got):
+    assert V.sha256(got) == case["outputs_sha256"][name], f"{case['id']}:{name}"
+    if case["stored"]:
+        np.testing.assert_array_equal(bits(got), bits(arrays[f"{case['id']}/{name}"]))
+
+
+@pytest.mark.parametrize("variant", list(VARIANTS))
+@pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
+def test_reduce_slab_bitwise(case, variant, dev, golden):
+    from fedsim_amd import ops
+
+    _, arrays = golden
+    X = _inputs(case)
+    idx, ws, W, _ = ref.accepted(case["weights"])
+    Xd = torch.from_numpy(np.ascontiguousarray(X[idx])).to(dev)
+    w32 = torch.tensor([ops.fl32(w) for w in ws], dtype=torch.float32, device=dev)
+    out = torch.empty(case["P"], dtype=torch.float32, device=dev)
+    fl = ops.tuning_flags(**VARIANTS[variant])
+    ops.reduce_slab(Xd, w32, out, flags=fl)
+    _expect(case, arrays, "sum", out.cpu().numpy())
+    ops.reduce_slab(Xd, w32, out, W=W, flags=fl)
+    _expect(case, arrays, "avg", out.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
+def test_reduce_rows_and_batches_bitwise(case, dev, golden):
+    """Row-table kernel, and the reduction split into batches chained through
+    the accumulator, both equal the single-pass reference result."""
+    from fedsim_amd import ops
+
+    _, arrays = golden
+    X = _inputs(case)
+    idx, ws, W, _ = ref.accepted(case["weights"])
+    rows = [torch.from_numpy(X[k].copy()).to(dev) for k in idx]
+    w32 = torch.tensor([ops.fl32(w) for w in ws], dtype=torch.float32, device=dev)
+    out = torch.empty(case["P"], dtype=torch.float32, device=dev)
+    ops.reduce_rows(rows, w32, out, W=W)
+    _expect(case, arrays, "avg", out.cpu().numpy())
+    # batches of 1, 2, 3, ... rows, finalize fused into the last batch
+    acc = torch.empty_like(out)
+    k0, b = 0, 1
+    first = True
+    while k0 < len(rows):
+        k1 = min(len(rows), k0 + b)
+        last = k1 == len(rows)
+        ops.reduce_rows(rows[k0:k1], w32[k0:k1].contiguous(), acc,
+                        acc_in=None if first else acc, W=W if last else None)
+        first, k0, b = False, k1, b + 1
+    _expect(case, arrays, "avg", acc.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
+def test_epilogues_bitwise(case, dev, golden):
+    from fedsim_amd import ops
+
+    _, arrays = golden
+    X = _inputs(case)
+    idx, ws, W, _ = ref.accepted(case["weights"])
+    avg = torch.from_numpy(ref.reduce(X[idx], ws, W=W)).to(dev)
+    cloud0 = V.cloud_vector(case["P"], case["seed"] + 1)
+    for lr in case["lrs"]:
+        cloud = torch.from_numpy(cloud0.copy()).to(dev)
+        if case["algo"] == "adabest":
+            prev = torch.from_numpy(V.cloud_vector(case["P"], case["seed"] + 2)).to(dev)
+            ops.adabest_sgd(avg, cloud, prev, case["beta"], lr)
+            _expect(case, arrays, f"avg_params_lr{lr}", prev.cpu().numpy())
+        else:
+            ops.fedavg_sgd(avg, cloud, lr)
+        _expect(case, arrays, f"cloud_lr{lr}", cloud.cpu().numpy())
+
+
+def test_scalar_path_unaligned_rows(dev):
+    """Rows at a 4-byte (not 16-byte) offset take the generic kernel; same bits."""
+    from fedsim_amd import ops
+
+    K, P = 9, 1029
+    X = V.client_rows("normal", K, P + 1, 77)
+    w = V.client_weights("fedavg", K, 77)
+    big = torch.from_numpy(X).to(dev)
+    rows = [big[k, 1:] for k in range(K)]  # 4-byte misaligned views
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    ops.reduce_rows(rows, w32, out, W=sum(w))
+    exp = ref.reduce(np.ascontiguousarray(X[:, 1:]), w, W=sum(w))
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(exp))
+    ops.reduce_slab(big[:, 1:], w32, out, W=sum(w))
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(exp))
+
+
+def test_empty_inputs(dev):
+    from fedsim_amd import ops
+
+    w32 = torch.ones(1, dtype=torch.float32, device=dev)
+    # B = 0: writes +0.0 (and 0/W when finalizing)
+    out = torch.full((37,), 5.0, device=dev)
+    ops.reduce_slab(torch.empty((0, 37), device=dev), w32, out)
+    assert torch.equal(out.cpu(), torch.zeros(37))
+    # P = 0: no launch, no error
+    ops.reduce_slab(torch.empty((3, 0), device=dev), w32.repeat(3), torch.empty(0, device=dev))

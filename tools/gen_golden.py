@@ -70,26 +70,6 @@ def import_reference(ref_root):
     )
 
 
-def client_msgs(X, weights, diverged_at=None):
-    """Client messages shaped like FedAvg.send_to_server's return
-    (fedavg.py:173-179).  The train-split sample count carries the weight."""
-    msgs = []
-    for k in range(X.shape[0]):
-        w = weights[k]
-        n = w if isinstance(w, int) else int(round(w * 10))
-        msgs.append(
-            dict(
-                local_params=torch.from_numpy(X[k].copy()),
-                num_steps=max(1, n // 32),
-                diverged=(diverged_at is not None and k == diverged_at),
-                num_samples={"train": n, "test": 100 + k},
-                metrics={"train": {"loss": 2.0 + 0.01 * k, "acc": 0.1 * (k % 7)},
-                         "test": {"acc": 0.05 * (k % 5)}},
-            )
-        )
-    return msgs
-
-
 def run_case(R, case):
     K, P = case["K"], case["P"]
     X = V.client_rows(case["dist"], K, P, case["seed"])
@@ -99,7 +79,7 @@ def run_case(R, case):
         for z in zero_at:
             weights[z] = 0 if isinstance(weights[z], int) else 0.0
     algo = case["algo"]
-    msgs = client_msgs(X, weights, case.get("diverged_at"))
+    msgs = V.client_messages(X, weights, case.get("diverged_at"))
     storage = R["Storage"]()
     agg = R["SerialAggregator"]()
     app = R["AppendixAggregator"]()
@@ -136,7 +116,7 @@ def run_case(R, case):
         st.write("lr_scheduler", None)
         # each optimize consumes its aggregator: rebuild an identical one
         a2 = R["SerialAggregator"]()
-        for k, msg in enumerate(client_msgs(X, weights)):
+        for k, msg in enumerate(V.client_messages(X, weights)):
             if algo == "adabest":
                 R["serial_aggregation"](st, k, msg, "train", a2, train_weight=1)
             elif algo == "fednova":

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; steps are chained with && so the
+# first failure ends the session.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r01}
+mkdir -p "$OUT"
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+&& timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+&& timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
+&& timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
+     -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.log" 2>&1
+rc=$?
+echo "exit $rc"
+exit $rc
