@@ -1,0 +1,74 @@
+"""Synthetic federation for round-loop parity (TEST INFRASTRUCTURE ONLY).
+
+Used identically by tools/gen_golden_rounds.py (driving the REFERENCE's
+CentralFLAlgorithm._train, centralized_fl_algorithm.py:411-443) and by
+tests/test_gpu_roundloop.py (driving fedsim_amd's): a fake DataManager, a tiny
+model, and a deterministic ``send_to_server`` that returns
+``cloud + delta(client, round)`` so the multi-round trajectory depends on every
+aggregation and server step.  No datasets, no local training.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch import nn
+from torch.nn.utils import parameters_to_vector
+
+from . import vectors as V
+
+NUM_CLIENTS = 20
+SAMPLE_RATE = 0.25
+ROUNDS = 4  # train(rounds=4) runs 5 rounds (trange(rounds + 1), :415)
+RANDOM_SEED = 123
+TORCH_SEED = 0
+
+
+class FakeDataManager(object):
+    def __init__(self, num_clients=NUM_CLIENTS):
+        self.sizes = [int(v) for v in V.randint(4242, num_clients, 40, 400)]
+
+    def get_global_dataset(self):
+        return {}
+
+    def get_oracle_dataset(self):
+        return None
+
+    def get_local_dataset(self, client_id):
+        return {"train": list(range(self.sizes[client_id]))}
+
+    def get_local_splits_names(self):
+        return ["train"]
+
+
+class TinyModel(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.l1 = nn.Linear(37, 11)
+        self.l2 = nn.Linear(11, 3)
+
+    def forward(self, x):
+        return self.l2(torch.relu(self.l1(x)))
+
+
+def synthetic_send_to_server(id, rounds, storage, datasets, train_split_name, scores, epochs,
+                             criterion, train_batch_size, inference_batch_size, optimizer_def,
+                             lr_scheduler_def=None, device="cuda", ctx=None,
+                             step_closure=None):
+    model = ctx["model"]
+    base = parameters_to_vector(model.parameters()).detach().cpu()
+    delta = torch.from_numpy((0.01 * V.gauss(id * 7919 + rounds, base.numel())).astype(np.float32))
+    local = base + delta
+    n = len(datasets[train_split_name])
+    return dict(
+        local_params=local.to(device),
+        num_steps=max(1, n // 32),
+        diverged=False,
+        num_samples={train_split_name: n},
+        metrics={train_split_name: {"loss": 1.0 + 0.001 * id + 0.01 * rounds}},
+    )
+
+
+def make_algorithm(base_cls):
+    """Subclass of an algorithm class with the synthetic client side."""
+    return type("Synthetic" + base_cls.__name__, (base_cls,),
+                {"send_to_server": synthetic_send_to_server})
