@@ -42,8 +42,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--K", type=int, default=1000, help="clients per round")
     ap.add_argument("--P", type=int, default=25_000_000, help="params per GPU shard")
-    ap.add_argument("--unroll", type=int, default=4, choices=[0, 4, 8, 16])
-    ap.add_argument("--vpt", type=int, default=2, choices=[0, 1, 2])
+    ap.add_argument("--layout", default="blocked", choices=["blocked", "strided"],
+                    help="HBM slab layout (blocked: column blocks of C floats, rows "
+                         "contiguous inside a block; strided: row-major [K, ldx])")
+    ap.add_argument("--C", type=int, default=4096, choices=[1024, 2048, 4096])
+    ap.add_argument("--unroll", type=int, default=4, choices=[0, 2, 4, 8, 16])
+    ap.add_argument("--vpt", type=int, default=2, choices=[0, 1, 2, 4],
+                    help="float4 slots per lane (strided layout only)")
     ap.add_argument("--nt", type=int, default=1)
     ap.add_argument("--no-epilogue", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -66,32 +71,49 @@ def dist_setup():
     return world, rank, local, pg
 
 
-def make_inputs(K, P, rank, dev):
+def make_inputs(K, P, rank, dev, layout, C):
     """x_k = base + eps_k, base ~ N(0, 0.05) (seed 7), eps_k ~ N(0, 1e-3)
     (Philox, seed 20261015 + row block); FedAvg weights w_k ~ U{50..600}
-    (numpy seed 11).  Row-major [K, ldx] fp32 slab, 256-B aligned rows."""
-    ldx = (P + 63) // 64 * 64
-    X = torch.empty((K, ldx), dtype=torch.float32, device=dev)
+    (numpy seed 11).
+
+    strided: row-major [K, ldx] fp32 slab, 256-B aligned rows.
+    blocked: [ceil(P/C), K, C] — column block b holds rows 0..K-1 of columns
+             [bC, bC+C) contiguously (include/fedagg.h), the layout the
+             aggregator packs client vectors into."""
     g = torch.Generator(device=dev)
     g.manual_seed(7 + 1_000_003 * rank)
     base = torch.empty(P, dtype=torch.float32, device=dev).normal_(0.0, 0.05, generator=g)
     blk = 64
+    if layout == "strided":
+        ldx = (P + 63) // 64 * 64
+        X = torch.empty((K, ldx), dtype=torch.float32, device=dev)
+    else:
+        X = torch.zeros(ops.blocked_shape(K, P, C), dtype=torch.float32, device=dev)
+        tmp = torch.empty((blk, P), dtype=torch.float32, device=dev)
+        full = P // C
     for k0 in range(0, K, blk):
         k1 = min(K, k0 + blk)
         g.manual_seed(20261015 + k0 + 1_000_003 * rank)
-        X[k0:k1, :P].normal_(0.0, 1e-3, generator=g).add_(base)
+        if layout == "strided":
+            X[k0:k1, :P].normal_(0.0, 1e-3, generator=g).add_(base)
+        else:
+            t = tmp[: k1 - k0].normal_(0.0, 1e-3, generator=g).add_(base)
+            X[:full, k0:k1, :].copy_(t[:, : full * C].view(k1 - k0, full, C).transpose(0, 1))
+            if P % C:
+                X[full, k0:k1, : P % C].copy_(t[:, full * C:])
     del base
     weights = [int(v) for v in np.random.default_rng(11).integers(50, 601, size=K)]
     return X, weights
 
 
-def load_pmc(path, K, P, flags):
+def load_pmc(path, K, P, flags, layout):
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("K") == K and d.get("P") == P and d.get("flags") == flags:
+    if d.get("K") == K and d.get("P") == P and d.get("flags") == flags and \
+            d.get("layout", "strided") == layout:
         return d.get("hbm_bytes_per_launch")
     return None
 
@@ -140,19 +162,25 @@ def main():
     world, rank, local, dist = dist_setup()
     dev = torch.device("cuda", local)
     K, P = a.K, a.P
-    flags = ops.tuning_flags(unroll=a.unroll, vpt=a.vpt, nt=bool(a.nt))
-    X, weights = make_inputs(K, P, rank, dev)
+    flags = ops.tuning_flags(unroll=a.unroll, vpt=a.vpt if a.layout == "strided" else 0,
+                             nt=bool(a.nt))
+    X, weights = make_inputs(K, P, rank, dev, a.layout, a.C)
     W = sum(weights)
     w32 = torch.tensor([ops.fl32(v) for v in weights], dtype=torch.float32, device=dev)
     avg = torch.empty(P, dtype=torch.float32, device=dev)
     cloud = torch.zeros(P, dtype=torch.float32, device=dev)
-    Xv = X[:, :P]
     stream = torch.cuda.current_stream(dev)
+
+    def reduce():
+        if a.layout == "strided":
+            ops.reduce_slab(X[:, :P], w32, avg, W=W, P=P, flags=flags)
+        else:
+            ops.reduce_blocked(X, w32, avg, W=W, flags=flags)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        ops.reduce_slab(Xv, w32, avg, W=W, P=P, flags=flags)
+        reduce()
         if ev is not None:
             ev[1].record(stream)
         if not a.no_epilogue:
@@ -183,7 +211,8 @@ def main():
     value = total_bytes * a.steps / elapsed / 1e9
     alg_bytes_launch = 4.0 * K * P + 4.0 * P + 4.0 * K
     achieved = alg_bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_pmc(a.pmc_json, K, P, flags)
+    traffic = load_pmc(a.pmc_json, K, P, flags,
+                       a.layout if a.layout == "strided" else f"blocked{a.C}")
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -205,11 +234,13 @@ def main():
             "params_total": P * world,
             "parallelism": f"param-shard{world}" if world > 1 else "single",
             "mode": "exact (bitwise vs reference CPU)",
+            "layout": a.layout if a.layout == "strided" else f"blocked C={a.C}",
             "flags": flags,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_reduce_vec (fedagg_reduce_f32)",
+            "kernel": "k_reduce_vec (%s)" % (
+                "fedagg_reduce_blocked_f32" if a.layout == "blocked" else "fedagg_reduce_f32"),
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBPS,
             "unit": "GB/s",

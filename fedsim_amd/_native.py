@@ -49,6 +49,17 @@ SIGNATURES = {
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
          ctypes.c_void_p],
     ),
+    "fedagg_reduce_blocked_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
+         ctypes.c_void_p],
+    ),
+    "fedagg_pack_row_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_void_p],
+    ),
     "fedagg_finalize_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p,

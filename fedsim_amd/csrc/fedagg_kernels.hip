@@ -41,6 +41,9 @@
 namespace {
 
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
+// Tuned defaults (profiles/r01_*: K=1000 x P=25M sweep on MI355X).
+constexpr int kDefaultUnroll = 4;
+constexpr int kDefaultVptSel = 2;  // 2 float4 slots per lane
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).
@@ -54,6 +57,21 @@ struct RowsStrided {
   int64_t ldx;
   __device__ __forceinline__ const char* row(int64_t k) const {
     return reinterpret_cast<const char*>(X + k * ldx);
+  }
+};
+
+// Column-blocked slab: for column block b (C floats = one workgroup's span),
+// rows 0..Kcap-1 are contiguous, so a workgroup streams one contiguous
+// Kcap*C*4-byte region (TLB/DRAM-page friendly).  Element (k, p) lives at
+// X[((p / C) * Kcap + k) * C + p % C].  row(k) is biased by -b*C so that the
+// kernel's global slot offsets land inside block b's region.
+struct RowsBlocked {
+  const float* X;
+  int64_t Kcap;
+  int64_t C;
+  __device__ __forceinline__ const char* row(int64_t k) const {
+    return reinterpret_cast<const char*>(
+        X + (static_cast<int64_t>(blockIdx.x) * (Kcap - 1) + k) * C);
   }
 };
 
@@ -195,10 +213,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(Rows rows,
                                                        int tail, const float* acc_in,
                                                        float* out, float W32,
                                                        int flags) {
-  const int64_t block_end = static_cast<int64_t>(blockIdx.x + 1) * (kBlock * VPT);
+  const int64_t block_start = static_cast<int64_t>(blockIdx.x) * (kBlock * VPT);
+  const int64_t block_end = block_start + kBlock * VPT;
   if (block_end <= nvec) {
     reduce_vec_body<U, VPT, NT, false>(rows, w, B, nvec, acc_in, out, W32, flags);
-  } else if (nvec > 0) {
+  } else if (block_start < nvec) {
     reduce_vec_body<U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
   }
   // The last block also owns the (P % 4) scalar tail columns.
@@ -313,7 +332,9 @@ hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
                       hipStream_t s) {
   const int64_t nvec = P / 4;
   const int tail = static_cast<int>(P - nvec * 4);
-  int64_t grid = (nvec + kBlock * VPT - 1) / (kBlock * VPT);
+  // one workgroup per kBlock*VPT float4 slots; the scalar tail belongs to the
+  // workgroup whose column span contains it (matters for RowsBlocked)
+  int64_t grid = (nvec + (tail > 0 ? 1 : 0) + kBlock * VPT - 1) / (kBlock * VPT);
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((k_reduce_vec<U, VPT, NT, Rows>), dim3(static_cast<unsigned>(grid)),
                      dim3(kBlock), 0, s, rows, w, B, nvec, tail, acc_in, out, W32, flags);
@@ -326,10 +347,11 @@ hipError_t dispatch_unroll(int unroll_sel, const Rows& rows, const float* w, int
                            int flags, hipStream_t s) {
   switch (unroll_sel) {
     case 1: return launch_vec<4, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 2: return launch_vec<8, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
     case 3: return launch_vec<16, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 4: return launch_vec<2, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
     case 0:
-    case 2:
-    default: return launch_vec<8, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    default: return launch_vec<kDefaultUnroll, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
   }
 }
 
@@ -347,12 +369,18 @@ hipError_t dispatch_reduce(const Rows& rows, bool vec_ok, const float* w, int64_
   const int unroll_sel = (flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT;
   const int vpt_sel = (flags & FEDAGG_VPT_MASK) >> FEDAGG_VPT_SHIFT;
   const bool nt = (flags & FEDAGG_NT) != 0;
-  if (vpt_sel == 2) {
-    return nt ? dispatch_unroll<2, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-              : dispatch_unroll<2, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+  switch (vpt_sel == 0 ? kDefaultVptSel : vpt_sel) {
+    case 1:
+      return nt ? dispatch_unroll<1, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+                : dispatch_unroll<1, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+    case 3:
+      return nt ? dispatch_unroll<4, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+                : dispatch_unroll<4, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+    case 2:
+    default:
+      return nt ? dispatch_unroll<2, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+                : dispatch_unroll<2, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
   }
-  return nt ? dispatch_unroll<1, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-            : dispatch_unroll<1, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
 }
 
 int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
@@ -411,6 +439,64 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
   RowsTable tab{rows};
   return static_cast<int>(dispatch_reduce(tab, vec_ok, w, B, P, acc_in, out, W32, flags,
                                           static_cast<hipStream_t>(stream)));
+}
+
+int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
+                              int64_t B, int64_t P, const float* acc_in, float* out,
+                              float W32, int flags, void* stream) {
+  int rc = check_reduce_args(w, B, P, acc_in, out, flags);
+  if (rc != 0 || P == 0) return rc;
+  if (B > Kcap || (B > 0 && !Xb)) return FEDAGG_EINVAL;
+  if (!aligned16(Xb) || !aligned16(out) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in)))
+    return FEDAGG_EINVAL;
+  RowsBlocked rows{Xb, Kcap, C};
+  const int unroll_sel = (flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT;
+  const bool nt = (flags & FEDAGG_NT) != 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (C) {  // the column block is one workgroup's span: C = 256 lanes * VPT * 4
+    case 1024:
+      e = nt ? dispatch_unroll<1, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+             : dispatch_unroll<1, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+      break;
+    case 2048:
+      e = nt ? dispatch_unroll<2, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+             : dispatch_unroll<2, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+      break;
+    case 4096:
+      e = nt ? dispatch_unroll<4, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+             : dispatch_unroll<4, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+      break;
+    default:
+      return FEDAGG_EINVAL;
+  }
+  return static_cast<int>(e);
+}
+
+int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, int64_t C,
+                        int64_t r, void* stream) {
+  if (P < 0 || Kcap <= 0 || r < 0 || r >= Kcap) return FEDAGG_EINVAL;
+  if (C != 1024 && C != 2048 && C != 4096) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!src || !Xb) return FEDAGG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t full = P / C;
+  const int64_t rem = P - full * C;
+  float* dst = Xb + r * C;
+  // One 2-D DMA: `full` segments of C floats, source pitch C, destination
+  // pitch Kcap*C (the next column block of the same row), then the remainder.
+  if (full > 0) {
+    hipError_t e = hipMemcpy2DAsync(dst, static_cast<size_t>(Kcap * C) * 4, src,
+                                    static_cast<size_t>(C) * 4, static_cast<size_t>(C) * 4,
+                                    static_cast<size_t>(full), hipMemcpyDefault, s);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  if (rem > 0) {
+    hipError_t e = hipMemcpyAsync(dst + full * Kcap * C, src + full * C,
+                                  static_cast<size_t>(rem) * 4, hipMemcpyDefault, s);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return 0;
 }
 
 int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out, void* stream) {

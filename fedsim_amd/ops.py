@@ -40,10 +40,16 @@ def fl32(x) -> float:
 
 
 def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False) -> int:
-    sel = {0: 0, 4: 1, 8: 2, 16: 3}[unroll]
-    return (sel << _native.FEDAGG_UNROLL_SHIFT) | (vpt << _native.FEDAGG_VPT_SHIFT) | (
+    sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4}[unroll]
+    vsel = {0: 0, 1: 1, 2: 2, 4: 3}[vpt]
+    return (sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT) | (
         FEDAGG_NT if nt else 0
     )
+
+
+# Tuned default for the column-blocked reduce (profiles/r01_sweep_*): k-unroll 4,
+# non-temporal client-row loads; the float4 slots per lane follow from C.
+DEFAULT_FLAGS = tuning_flags(unroll=4, nt=True)
 
 
 def _stream_ptr(device: torch.device) -> int:
@@ -153,6 +159,95 @@ def reduce_rows(
     )
     check(rc, "fedagg_reduce_rows_f32")
     return out
+
+
+BLOCK_COLS = (1024, 2048, 4096)
+
+
+def blocked_shape(K: int, P: int, C: int = 2048):
+    """Shape [ceil(P/C), K, C] of a column-blocked slab (see fedagg.h)."""
+    if C not in BLOCK_COLS:
+        raise ValueError(f"C must be one of {BLOCK_COLS}")
+    return ((P + C - 1) // C, K, C)
+
+
+def to_blocked(X: torch.Tensor, C: int = 2048) -> torch.Tensor:
+    """Repack a [K, P] tensor into the column-blocked layout (copy)."""
+    K, P = X.shape
+    nb, _, _ = blocked_shape(K, P, C)
+    Xb = torch.zeros((nb, K, C), dtype=X.dtype, device=X.device)
+    full = P // C
+    if full:
+        Xb[:full].copy_(X[:, : full * C].reshape(K, full, C).transpose(0, 1))
+    if P % C:
+        Xb[full, :, : P % C].copy_(X[:, full * C:])
+    return Xb
+
+
+def reduce_blocked(
+    Xb: torch.Tensor,
+    w32: torch.Tensor,
+    out: torch.Tensor,
+    B: Optional[int] = None,
+    acc_in: Optional[torch.Tensor] = None,
+    W: Optional[float] = None,
+    flags: int = 0,
+    r0: int = 0,
+) -> torch.Tensor:
+    """Reduce rows r0..r0+B-1 of a column-blocked slab ``Xb`` ([nblk, Kcap, C])."""
+    _require_hip_f32(Xb, "Xb")
+    _require_hip_f32(w32, "w32")
+    _require_hip_f32(out, "out")
+    if Xb.dim() != 3 or not Xb.is_contiguous():
+        raise ValueError("Xb must be a contiguous [nblk, Kcap, C] tensor")
+    nb, Kcap, C = Xb.shape
+    P = out.numel()
+    if nb != (P + C - 1) // C:
+        raise ValueError("Xb block count does not match out's length")
+    B = Kcap - r0 if B is None else B
+    if w32.numel() < B:
+        raise ValueError("w32 too short")
+    if r0 < 0 or B < 0 or r0 + B > Kcap:
+        raise ValueError("row range outside the slab")
+    f = flags
+    if acc_in is None:
+        f |= FEDAGG_INIT
+    else:
+        _require_hip_f32(acc_in, "acc_in")
+    W32 = 0.0
+    if W is not None:
+        f |= FEDAGG_FINALIZE
+        W32 = fl32(W)
+    rc = _native.load().fedagg_reduce_blocked_f32(
+        Xb.data_ptr() + 4 * r0 * C, Kcap, C, w32.data_ptr(), B, P, _ptr(acc_in),
+        out.data_ptr(), W32, f, _stream_ptr(out.device),
+    )
+    check(rc, "fedagg_reduce_blocked_f32")
+    return out
+
+
+def pack_row(src: torch.Tensor, Xb: torch.Tensor, r: int, stream=None) -> None:
+    """Copy one client vector (contiguous fp32; pinned host or HIP memory) into
+    row ``r`` of the column-blocked slab ``Xb`` with one 2-D DMA, ordered on
+    ``stream`` (default: the current stream of Xb's device).
+
+    The DMA is asynchronous and bypasses torch's copy bookkeeping: the caller
+    keeps ``src`` alive and unmodified until ``stream`` has passed the copy
+    (the aggregator's staging ring does this with per-slot events)."""
+    _require_hip_f32(Xb, "Xb")
+    if not isinstance(src, torch.Tensor) or src.dtype != torch.float32:
+        raise TypeError("src must be a float32 tensor")
+    if not src.is_contiguous():
+        raise ValueError("src must be contiguous")
+    if src.device.type == "cuda" and src.device != Xb.device:
+        raise ValueError("device src must live on Xb's device")
+    nb, Kcap, C = Xb.shape
+    P = src.numel()
+    if nb != (P + C - 1) // C or not 0 <= r < Kcap:
+        raise ValueError("src / slab shape mismatch")
+    s = stream.cuda_stream if stream is not None else _stream_ptr(Xb.device)
+    rc = _native.load().fedagg_pack_row_f32(src.data_ptr(), P, Xb.data_ptr(), Kcap, C, r, s)
+    check(rc, "fedagg_pack_row_f32")
 
 
 def finalize(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.Tensor:

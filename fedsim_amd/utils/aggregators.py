@@ -5,15 +5,18 @@ reference's ``SerialAggregator`` (fedsim/utils/aggregators.py:11-144) whose
 tensor-valued keys are reduced on the MI355X by libfedagg:
 
 * ``add(key, tensor, weight)`` (aggregators.py:23-40) snapshots the client
-  vector into a chunked HBM slab (H2D for CPU tensors, D2D for HIP tensors) and
-  records ``fl32(weight)``; the running weight is the same Python sum
-  ``cur_w + weight`` as the reference (so ``weight=None`` raises the same
-  TypeError).  Full slabs are reduced by the exact-mode kernel into an fp32
-  accumulator in arrival order.
-* ``get`` / ``pop`` (aggregators.py:42-60, 104-122) reduce the pending rows and,
-  when the weight is non-zero, divide by ``fl32(W)`` inside the same kernel
-  pass.  The result is bit-identical to the reference CPU aggregation and is
-  returned on the device the values came from (CPU in, CPU out).
+  vector into a column-blocked HBM ring slab and records ``fl32(weight)``; the
+  running weight is the same Python sum ``cur_w + weight`` as the reference (so
+  ``weight=None`` raises the same TypeError).  HIP-resident vectors are packed
+  with a D2D 2-D DMA on the compute stream; host vectors are snapshotted into a
+  pinned staging ring and DMA'd on a separate copy stream, overlapping the
+  reductions.
+* Pending rows are reduced by the exact-mode kernel into an fp32 accumulator in
+  arrival order whenever the ring needs room, and at ``get`` / ``pop``
+  (aggregators.py:42-60, 104-122), where the divide by ``fl32(W)`` is fused
+  into the same kernel pass.  Results are bit-identical to the reference CPU
+  aggregation and come back on the device the values came from (CPU in, CPU
+  out).
 * ``get_sum`` / ``get_weight`` / ``keys`` / ``items`` / ``pop_all`` /
   ``__contains__`` keep the reference semantics; a missing key raises
   ``Exception(f"{key} is not in the aggregator")``.
@@ -39,7 +42,8 @@ __all__ = ["SerialAggregator", "DeviceAggregator", "AppendixAggregator"]
 
 _DEFAULT_SLAB_BYTES = int(os.environ.get("FEDSIM_AMD_SLAB_BYTES", 16 << 30))
 _DEFAULT_MAX_ROWS = int(os.environ.get("FEDSIM_AMD_MAX_ROWS", 4096))
-_ROW_ALIGN = 64  # fp32 elements: 256-B aligned slab rows
+_BLOCK_COLS = 4096  # columns per workgroup span in the blocked slab (sweep: fastest)
+_STAGING_SLOTS = 3
 
 
 def _hip_device(value: torch.Tensor, device) -> torch.device:
@@ -55,41 +59,113 @@ def _hip_device(value: torch.Tensor, device) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+class _Ingest(object):
+    """Pinned staging ring + copy stream for host-resident client vectors.
+
+    ``put`` copies the vector into a pinned slot on the CPU (that copy is the
+    reference's snapshot: the caller may reuse its tensor as soon as add
+    returns), then DMAs the slot into the slab row on the copy stream.  A slot
+    is reused only after its previous DMA has completed."""
+
+    def __init__(self, dev: torch.device, nslots: int = _STAGING_SLOTS):
+        self.dev = dev
+        self.stream = torch.cuda.Stream(device=dev)
+        self.bufs: List[Optional[torch.Tensor]] = [None] * nslots
+        self.events: List[Optional[torch.cuda.Event]] = [None] * nslots
+        self.i = 0
+
+    def put(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None):
+        if src.is_pinned():
+            # DMA straight from the caller's pinned buffer; the snapshot is
+            # complete once the DMA is, so wait for it before returning.
+            if wait_event is not None:
+                self.stream.wait_event(wait_event)
+            ops.pack_row(src, Xb, r, stream=self.stream)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            ev.synchronize()
+            return ev
+        i = self.i % len(self.bufs)
+        self.i += 1
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        P = src.numel()
+        buf = self.bufs[i]
+        if buf is None or buf.numel() < P:
+            buf = torch.empty(max(P, 1), dtype=torch.float32, pin_memory=True)
+            self.bufs[i] = buf
+        slot = buf[:P]
+        slot.copy_(src)
+        if wait_event is not None:
+            self.stream.wait_event(wait_event)
+        ops.pack_row(slot, Xb, r, stream=self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self.events[i] = ev
+        return ev
+
+
+class _Options(object):
+    __slots__ = ("device", "slab_bytes", "max_rows", "flags", "expected_rows", "block_cols")
+
+    def __init__(self, device, slab_bytes, max_rows, flags, expected_rows, block_cols):
+        self.device = device
+        self.slab_bytes = slab_bytes
+        self.max_rows = max_rows
+        self.flags = flags
+        self.expected_rows = expected_rows
+        self.block_cols = block_cols
+
+
 class _DeviceEntry(object):
-    """One tensor-valued key: fp32 running sum in HBM + pending client rows."""
+    """One tensor-valued key: fp32 running sum in HBM + a ring of pending
+    client rows in a column-blocked slab [ceil(P/C), R, C] (include/fedagg.h)."""
 
-    __slots__ = ("shape", "P", "ldx", "out_device", "dev", "acc", "cur_w", "chunks",
-                 "rows_total", "n_pending", "pending_w", "max_rows", "flags")
-
-    def __init__(self, value: torch.Tensor, dev: torch.device, slab_bytes: int,
-                 max_rows: int, flags: int):
+    def __init__(self, value: torch.Tensor, dev: torch.device, opts: _Options, agg):
         self.shape = tuple(value.shape)
         self.P = value.numel()
-        self.ldx = (self.P + _ROW_ALIGN - 1) // _ROW_ALIGN * _ROW_ALIGN
         self.out_device = value.device
         self.dev = dev
-        self.acc: Optional[torch.Tensor] = None
-        self.cur_w = 0
-        self.chunks: List[torch.Tensor] = []
-        self.rows_total = 0
+        self.C = opts.block_cols
+        self.nblk = (self.P + self.C - 1) // self.C
+        row_bytes = 4 * max(1, self.nblk) * self.C
+        self.Rmax = max(2, min(opts.max_rows, opts.slab_bytes // row_bytes))
+        self.R = 0
+        self.slab: Optional[torch.Tensor] = None
+        self.hint = opts.expected_rows
+        self.flags = opts.flags
+        self.agg = agg
+        self.head = 0
+        self.tail = 0
         self.n_pending = 0
         self.pending_w: List[float] = []
-        row_bytes = 4 * max(self.ldx, 1)
-        self.max_rows = max(1, min(max_rows, slab_bytes // row_bytes))
-        self.flags = flags
+        self.acc: Optional[torch.Tensor] = None
+        self.cur_w = 0
+        self.copy_event = None       # last host DMA into the slab (copy stream)
+        self.last_flush_event = None  # last reduction reading the slab (compute stream)
+        self.wait_before_copy = None
 
-    # -- slab management ---------------------------------------------------
-    def _row(self, i: int) -> torch.Tensor:
-        for ch in self.chunks:
-            if i < ch.shape[0]:
-                return ch[i]
-            i -= ch.shape[0]
-        raise IndexError(i)
+    # -- ring management -----------------------------------------------------
+    def _alloc(self, rows: int) -> None:
+        self.slab = torch.empty((self.nblk, rows, self.C), dtype=torch.float32, device=self.dev)
+        self.R = rows
+        self.head = self.tail = 0
+        # a recycled block may still be read by an earlier reduction: the first
+        # host DMA into the new slab waits for the latest one
+        self.wait_before_copy = self.last_flush_event
 
-    def _grow(self) -> None:
-        n = min(max(8, self.rows_total), self.max_rows - self.rows_total)
-        self.chunks.append(torch.empty((n, self.ldx), dtype=torch.float32, device=self.dev))
-        self.rows_total += n
+    def _make_room(self) -> None:
+        if self.slab is None:
+            first = self.hint if self.hint else 8
+            self._alloc(min(self.Rmax, max(1, first)))
+            return
+        if self.R < self.Rmax:
+            if self.n_pending == self.R:
+                self._flush(final_W=None)
+                self._alloc(min(self.Rmax, 2 * self.R))
+        elif self.n_pending >= max(1, self.Rmax // 2):
+            # double buffering: drain one half while the other half fills
+            self._flush(final_W=None)
 
     # -- reference semantics -------------------------------------------------
     def add(self, value: torch.Tensor, weight) -> None:
@@ -101,38 +177,55 @@ class _DeviceEntry(object):
         if value.dtype != torch.float32:
             raise TypeError(f"device aggregation supports float32 tensors, got {value.dtype}")
         w32 = float(np.float32(weight))
-        if self.n_pending == self.max_rows:
-            self._flush(final_W=None)
-        if self.n_pending == self.rows_total:
-            self._grow()
-        dst = self._row(self.n_pending)[: self.P]
+        self._make_room()
+        r = self.head
         src = value.detach().reshape(-1)
-        # Snapshot now (the reference computes value * weight at add time).
-        # Pinned CPU sources are copied synchronously so the caller may reuse them.
-        dst.copy_(src, non_blocking=False)
-        self.pending_w.append(w32)
+        if src.device.type == "cuda":
+            if src.device != self.dev:
+                src = src.to(self.dev)
+            ops.pack_row(src.contiguous(), self.slab, r)  # D2D on the compute stream
+        else:
+            self.copy_event = self.agg._ingest(self.dev).put(
+                src.contiguous(), self.slab, r, wait_event=self.wait_before_copy)
+            self.wait_before_copy = None
+        self.head = (r + 1) % self.R
         self.n_pending += 1
+        self.pending_w.append(w32)
         self.cur_w = new_w
 
     def _flush(self, final_W) -> None:
-        """Reduce pending rows into acc; divide by fl32(final_W) if given."""
+        """Reduce the pending rows into acc (arrival order); divide by
+        fl32(final_W) in the same pass if given."""
         n = self.n_pending
+        cur = torch.cuda.current_stream(self.dev)
         if n == 0:
             if final_W is not None and self.acc is not None:
                 ops.finalize(self.acc, final_W, out=self.acc)
             return
+        if self.copy_event is not None:
+            cur.wait_event(self.copy_event)
+            self.copy_event = None
         if self.acc is None:
             self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
             acc_in = None
         else:
             acc_in = self.acc
-        rows = [self._row(i)[: self.P] for i in range(n)]
         w32 = torch.tensor(self.pending_w, dtype=torch.float32).pin_memory()
         w32 = w32.to(self.dev, non_blocking=True)
-        table = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).pin_memory()
-        table = table.to(self.dev, non_blocking=True)
-        ops.reduce_rows(rows, w32, self.acc, acc_in=acc_in, W=final_W, flags=self.flags,
-                        table=table)
+        first = self.R - self.tail
+        segs = [(self.tail, n)] if n <= first else [(self.tail, first), (0, n - first)]
+        off = 0
+        for i, (r0, cnt) in enumerate(segs):
+            last = i == len(segs) - 1
+            ops.reduce_blocked(self.slab, w32[off:off + cnt], self.acc, B=cnt, acc_in=acc_in,
+                               W=final_W if last else None, flags=self.flags, r0=r0)
+            acc_in = self.acc
+            off += cnt
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self.last_flush_event = ev
+        self.wait_before_copy = ev
+        self.tail = (self.tail + n) % self.R
         self.n_pending = 0
         self.pending_w = []
 
@@ -158,7 +251,7 @@ class _DeviceEntry(object):
     def pop(self, on_device: bool = False) -> torch.Tensor:
         self._flush(final_W=self.cur_w if self._weighted() else None)
         out = self.acc.view(self.shape) if on_device else self._deliver(self.acc)
-        self.chunks = []
+        self.slab = None
         self.acc = None
         return out
 
@@ -170,19 +263,28 @@ class SerialAggregator(object):
     Args:
         device: HIP device for tensor keys (default: the tensor's own device if
             it is a HIP tensor, else the current HIP device).
-        slab_bytes: HBM budget for pending client rows per key; when full, the
-            rows are reduced into the accumulator (order is preserved).
-        max_rows: cap on pending rows per key.
-        flags: libfedagg tuning flags (see include/fedagg.h).
+        slab_bytes: HBM budget of the pending-row ring per key; when it fills,
+            pending rows are reduced into the accumulator (order is preserved).
+        max_rows: cap on ring rows per key.
+        flags: libfedagg tuning flags (include/fedagg.h); default = tuned.
+        expected_rows: hint (e.g. clients per round) to size the ring once.
+        block_cols: column-block width C of the slab (1024 / 2048 / 4096).
     """
 
     def __init__(self, device=None, slab_bytes: int = _DEFAULT_SLAB_BYTES,
-                 max_rows: int = _DEFAULT_MAX_ROWS, flags: int = 0) -> None:
+                 max_rows: int = _DEFAULT_MAX_ROWS, flags: Optional[int] = None,
+                 expected_rows: Optional[int] = None, block_cols: int = _BLOCK_COLS) -> None:
         self._members: Dict = dict()
-        self._device = device
-        self._slab_bytes = slab_bytes
-        self._max_rows = max_rows
-        self._flags = flags
+        self._opts = _Options(device, slab_bytes, max_rows,
+                              ops.DEFAULT_FLAGS if flags is None else flags,
+                              expected_rows, block_cols)
+        self._ingests: Dict = {}
+
+    def _ingest(self, dev) -> _Ingest:
+        ing = self._ingests.get(dev)
+        if ing is None:
+            ing = self._ingests[dev] = _Ingest(dev)
+        return ing
 
     @staticmethod
     def _is_device_value(value) -> bool:
@@ -196,8 +298,8 @@ class SerialAggregator(object):
             entry.add(value, weight)
             return
         if entry is None and self._is_device_value(value):
-            dev = _hip_device(value, self._device)
-            entry = _DeviceEntry(value, dev, self._slab_bytes, self._max_rows, self._flags)
+            dev = _hip_device(value, self._opts.device)
+            entry = _DeviceEntry(value, dev, self._opts, self)
             entry.add(value, weight)
             self._members[key] = entry
             return

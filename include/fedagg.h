@@ -12,6 +12,8 @@
  *        serial_aggregation fedsim/distributed/centralized/training/utils.py:45-46)
  *       and, with FEDAGG_FINALIZE, SerialAggregator.get/pop's  v / w
  *                                                  fedsim/utils/aggregators.py:56-60,118-122
+ *   fedagg_reduce_blocked_f32
+ *       same, over a column-blocked HBM slab layout
  *   fedagg_finalize_f32
  *       replaces SerialAggregator.get/pop's v / w  fedsim/utils/aggregators.py:56-60,118-122
  *   fedagg_fedavg_sgd_f32
@@ -52,10 +54,10 @@ extern "C" {
 #define FEDAGG_FINALIZE  0x2  /* store fl32(acc / W32) instead of the raw sum              */
 #define FEDAGG_NT        0x4  /* non-temporal (streaming) loads of the client rows         */
 #define FEDAGG_SCALAR    0x8  /* force the 4-byte-per-lane path (rows not 16-B aligned)    */
-/* bits 8..11: k-unroll selector, 0 = library default, 1 = 4, 2 = 8, 3 = 16 */
+/* bits 8..11: k-unroll selector, 0 = library default, 1 = 4, 2 = 8, 3 = 16, 4 = 2 */
 #define FEDAGG_UNROLL_SHIFT 8
 #define FEDAGG_UNROLL_MASK  0xF00
-/* bits 12..13: float4 columns per thread, 0 = default, 1 = 1, 2 = 2 */
+/* bits 12..13: float4 slots per lane, 0 = library default, 1 = 1, 2 = 2, 3 = 4 */
 #define FEDAGG_VPT_SHIFT 12
 #define FEDAGG_VPT_MASK  0x3000
 
@@ -100,6 +102,30 @@ int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B,
 int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B,
                            int64_t P, const float* acc_in, float* out, float W32,
                            int flags, void* stream);
+
+/*
+ * Same reduction over a COLUMN-BLOCKED slab: columns are cut into blocks of C
+ * floats (C = 1024, 2048 or 4096, one workgroup's span) and, inside a block,
+ * the Kcap rows are contiguous:  element (k, p) is at
+ *     Xb[((p / C) * Kcap + k) * C + (p % C)],   Xb sized ceil(P / C) * Kcap * C.
+ * Each workgroup then streams one contiguous region instead of K strided
+ * 100-MB-apart rows.  Rows 0..B-1 (B <= Kcap) are reduced; rows r0..r0+B-1
+ * of a slab are reduced by passing Xb + r0*C (same Kcap), which is how a ring
+ * of client rows is drained in arrival order.
+ */
+int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
+                              int64_t B, int64_t P, const float* acc_in, float* out,
+                              float W32, int flags, void* stream);
+
+/*
+ * Pack one client vector (P contiguous fp32, host-pinned or device memory)
+ * into row r of a column-blocked slab [ceil(P/C), Kcap, C] with one 2-D DMA.
+ * This is the HBM side of SerialAggregator.add's snapshot (the reference's
+ * clone at fedsim/distributed/centralized/training/utils.py:34) and of
+ * vectorize_module's packing (fedsim/utils/convert_parameters.py:78-94).
+ */
+int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, int64_t C,
+                        int64_t r, void* stream);
 
 /* out[p] = fl32(acc[p] / W32)  (IEEE true division; out may alias acc). */
 int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out,

@@ -42,8 +42,9 @@ def lib():
         L.ref_finalize_f32.argtypes = [vp, f32, i64, vp]
         L.ref_fedavg_sgd_f32.argtypes = [vp, f32, vp, vp, i64]
         L.ref_adabest_sgd_f32.argtypes = [vp, f32, f32, vp, vp, vp, i64]
+        L.ref_feddyn_sgd_f32.argtypes = [vp, f32, f32, vp, vp, vp, vp, i64]
         for fn in ("ref_reduce_f32", "ref_finalize_f32", "ref_fedavg_sgd_f32",
-                   "ref_adabest_sgd_f32"):
+                   "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32"):
             getattr(L, fn).restype = None
         _lib = L
     return _lib
@@ -109,6 +110,18 @@ def adabest_sgd(avg: np.ndarray, cloud: np.ndarray, avg_prev: np.ndarray, beta: 
     lib().ref_adabest_sgd_f32(_p(a), float(fl32(beta)), float(fl32(lr)), _p(c), _p(ap), None,
                               c.size)
     return c, ap
+
+
+def feddyn_sgd(avg: np.ndarray, cloud: np.ndarray, h: np.ndarray, weight, num_clients,
+               lr: float):
+    """Returns (cloud', h', avg_params')."""
+    c = np.array(cloud, dtype=np.float32, copy=True)
+    hh = np.array(h, dtype=np.float32, copy=True)
+    a = np.ascontiguousarray(avg, dtype=np.float32)
+    ap = np.empty_like(c)
+    lib().ref_feddyn_sgd_f32(_p(a), float(fl32(weight / num_clients)), float(fl32(lr)), _p(c),
+                             _p(hh), _p(ap), None, c.size)
+    return c, hh, ap
 
 
 # ---- numpy twin (independent restatement of the reduce / divide) ----------

@@ -135,3 +135,46 @@ def test_empty_inputs(dev):
     assert torch.equal(out.cpu(), torch.zeros(37))
     # P = 0: no launch, no error
     ops.reduce_slab(torch.empty((3, 0), device=dev), w32.repeat(3), torch.empty(0, device=dev))
+
+
+@pytest.mark.parametrize("C", [1024, 2048, 4096])
+@pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
+def test_reduce_blocked_bitwise(case, C, dev, golden):
+    """Column-blocked slab layout (packed with the 2-D DMA), whole slab and as
+    a ring drained in two row ranges, equals the reference bitwise."""
+    from fedsim_amd import ops
+
+    _, arrays = golden
+    X = _inputs(case)
+    idx, ws, W, _ = ref.accepted(case["weights"])
+    B, P = len(idx), case["P"]
+    Xb = torch.full(ops.blocked_shape(B + 3, P, C), float("nan"), device=dev)
+    host = torch.from_numpy(np.ascontiguousarray(X[idx])).pin_memory()
+    for j in range(B):  # rows 2..B+1 of a B+3-row slab; odd rows from the host
+        src = host[j] if j % 2 else host[j].to(dev)
+        ops.pack_row(src, Xb, j + 2)
+    w32 = torch.tensor([ops.fl32(w) for w in ws], dtype=torch.float32, device=dev)
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    for variant in ("default", "u4v2nt", "u8v1"):
+        fl = ops.tuning_flags(**{k: v for k, v in VARIANTS[variant].items() if k != "vpt"})
+        ops.reduce_blocked(Xb, w32, out, B=B, W=W, flags=fl, r0=2)
+        _expect(case, arrays, "avg", out.cpu().numpy())
+    h = B // 2
+    ops.reduce_blocked(Xb, w32[:h].contiguous(), out, B=h, r0=2)
+    ops.reduce_blocked(Xb, w32[h:].contiguous(), out, B=B - h, acc_in=out, W=W, r0=2 + h)
+    _expect(case, arrays, "avg", out.cpu().numpy())
+
+
+def test_pack_row_layout(dev):
+    from fedsim_amd import ops
+
+    for P in (1, 5, 4095, 4096, 4097, 9000):
+        K, C = 3, 4096
+        X = torch.randn(K, P)
+        Xb = torch.zeros(ops.blocked_shape(K, P, C), device=dev)
+        srcs = [X[k].contiguous().pin_memory() for k in range(K)]  # alive until synced
+        for k in range(K):
+            ops.pack_row(srcs[k], Xb, k)
+        torch.cuda.synchronize()
+        ref_b = ops.to_blocked(X.to(dev), C)
+        assert torch.equal(Xb, ref_b)

@@ -52,6 +52,11 @@ def test_oracle_optimize_matches_reference(case, golden):
             prev0 = V.cloud_vector(case["P"], case["seed"] + 2)
             c, ap = ref.adabest_sgd(avg, cloud0, prev0, case["beta"], lr)
             _check(case, arrays, f"avg_params_lr{lr}", ap)
+        elif case["algo"] == "feddyn":
+            h0 = V.cloud_vector(case["P"], case["seed"] + 3)
+            c, h, ap = ref.feddyn_sgd(avg, cloud0, h0, W, case["num_clients"], lr)
+            _check(case, arrays, f"h_lr{lr}", h)
+            _check(case, arrays, f"avg_params_lr{lr}", ap)
         else:
             c = ref.fedavg_sgd(avg, cloud0, lr)
         _check(case, arrays, f"cloud_lr{lr}", c)

@@ -66,6 +66,7 @@ def import_reference(ref_root):
         FedAvg=training.FedAvg,
         AdaBest=training.AdaBest,
         FedNova=training.FedNova,
+        FedDyn=training.FedDyn,
         serial_aggregation=tutils.serial_aggregation,
     )
 
@@ -89,7 +90,7 @@ def run_case(R, case):
             # FedNova weight = n / num_steps (fednova.py:58-59); use the
             # prepared float weight directly via train_weight
             ok = R["serial_aggregation"](storage, k, msg, "train", agg, train_weight=weights[k])
-        elif algo == "adabest":
+        elif algo in ("adabest", "feddyn"):
             ok = R["serial_aggregation"](storage, k, msg, "train", agg, train_weight=1)
         else:
             ok = R["FedAvg"].receive_from_client(storage, k, msg, "train", agg, app)
@@ -117,7 +118,7 @@ def run_case(R, case):
         # each optimize consumes its aggregator: rebuild an identical one
         a2 = R["SerialAggregator"]()
         for k, msg in enumerate(V.client_messages(X, weights)):
-            if algo == "adabest":
+            if algo in ("adabest", "feddyn"):
                 R["serial_aggregation"](st, k, msg, "train", a2, train_weight=1)
             elif algo == "fednova":
                 R["serial_aggregation"](st, k, msg, "train", a2, train_weight=weights[k])
@@ -128,6 +129,12 @@ def run_case(R, case):
             st.write("avg_params", torch.from_numpy(avg_prev0.copy()))
             st.write("beta", case["beta"])
             reports = R["AdaBest"].optimize(st, a2, R["AppendixAggregator"]())
+            out["arrays"][f"avg_params_lr{lr}"] = st.read("avg_params").numpy().copy()
+        elif algo == "feddyn":
+            st.write("h", torch.from_numpy(V.cloud_vector(P, case["seed"] + 3)))
+            st.write("num_clients", case["num_clients"])
+            reports = R["FedDyn"].optimize(st, a2, R["AppendixAggregator"]())
+            out["arrays"][f"h_lr{lr}"] = st.read("h").numpy().copy()
             out["arrays"][f"avg_params_lr{lr}"] = st.read("avg_params").numpy().copy()
         else:
             reports = R["FedAvg"].optimize(st, a2, R["AppendixAggregator"]())
@@ -157,6 +164,8 @@ def build_cases():
         add(K=K, P=P, dist="realistic", wkind="adabest", algo="adabest", beta=0.6,
             lrs=[1.0, 0.3])
         add(K=K, P=P, dist="normal", wkind="fednova", algo="fednova", lrs=[1.0])
+        add(K=K, P=P, dist="realistic", wkind="adabest", algo="feddyn", num_clients=37,
+            lrs=[1.0, 0.3])
         add(K=K, P=P, dist="special", wkind="fedavg", algo="fedavg", lrs=[1.0, 0.3])
         add(K=K, P=P, dist="normal", wkind="bigint", algo="fedavg", lrs=[1.0])
     # edge cases of serial_aggregation (utils.py:39-46)
@@ -168,6 +177,8 @@ def build_cases():
     add(K=5, P=199_210, dist="realistic", wkind="fedavg", algo="fedavg", lrs=[1.0])
     add(K=10, P=1_085_668, dist="realistic", wkind="fedavg", algo="fedavg", lrs=[1.0])
     add(K=10, P=1_085_668, dist="realistic", wkind="adabest", algo="adabest", beta=0.6, lrs=[1.0])
+    add(K=10, P=1_085_668, dist="realistic", wkind="adabest", algo="feddyn", num_clients=1000,
+        lrs=[1.0])
     return cases
 
 

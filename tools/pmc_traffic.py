@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--K", type=int, required=True)
     ap.add_argument("--P", type=int, required=True)
     ap.add_argument("--flags", type=int, required=True)
+    ap.add_argument("--layout", default="blocked4096", help="strided | blocked<C>")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                   "pmc_traffic.json"))
     a = ap.parse_args()
@@ -50,7 +51,7 @@ def main():
     write_b = w_kib * 1024
     alg = 4.0 * a.K * a.P + 4.0 * a.P + 4.0 * a.K
     out = dict(
-        kernel=KERNEL, K=a.K, P=a.P, flags=a.flags,
+        kernel=KERNEL, K=a.K, P=a.P, flags=a.flags, layout=a.layout,
         dispatches=dict(fetch=len(fetch), write=len(write)),
         FETCH_SIZE_KiB_mean=f_kib, WRITE_SIZE_KiB_mean=w_kib,
         fetch_bytes_corrected=fetch_b, write_bytes=write_b,
