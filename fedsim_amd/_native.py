@@ -30,6 +30,7 @@ FEDAGG_NT = 0x4
 FEDAGG_SCALAR = 0x8
 FEDAGG_UNROLL_SHIFT = 8
 FEDAGG_VPT_SHIFT = 12
+FEDAGG_BS_SHIFT = 14
 FEDAGG_EINVAL = -22
 
 # (name, restype, argtypes) for every symbol include/fedagg.h declares.
@@ -73,6 +74,11 @@ SIGNATURES = {
     "fedagg_adabest_sgd_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p],
+    ),
+    "fedagg_feddyn_sgd_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p],
     ),
 }

@@ -44,6 +44,7 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // Tuned defaults (profiles/r01_*: K=1000 x P=25M sweep on MI355X).
 constexpr int kDefaultUnroll = 4;
 constexpr int kDefaultVptSel = 2;  // 2 float4 slots per lane
+constexpr int kDefaultBsSel = 1;   // blocked layout: 256-lane workgroups
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).
@@ -128,22 +129,22 @@ __device__ __forceinline__ f32x4 div4(f32x4 a, float d) {
 
 // ---------------------------------------------------------------------------
 // Exact-mode reduction, f32x4 slots.
-//   slot s covers columns [4s, 4s+4).  Block b owns slots
-//   [b*256*VPT, (b+1)*256*VPT); lane t of the block owns s = base + j*256 + t
+//   slot s covers columns [4s, 4s+4).  Block b (BS lanes) owns slots
+//   [b*BS*VPT, (b+1)*BS*VPT); lane t of the block owns s = base + j*BS + t
 //   for j < VPT, so every wave-instruction touches 64 consecutive slots (1 KiB).
 // ---------------------------------------------------------------------------
-template <int U, int VPT, bool NT, bool GUARD, class Rows>
+template <int BS, int U, int VPT, bool NT, bool GUARD, class Rows>
 __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
                                                 const float* __restrict__ w,
                                                 int64_t B, int64_t nvec,
                                                 const float* acc_in, float* out,
                                                 float W32, int flags) {
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * (kBlock * VPT) + threadIdx.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * (BS * VPT) + threadIdx.x;
   uint32_t off[VPT];
   bool ok[VPT];
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
-    int64_t s = base + j * kBlock;
+    int64_t s = base + j * BS;
     ok[j] = GUARD ? (s < nvec) : true;
     if (GUARD && !ok[j]) s = nvec - 1;  // clamp: load something valid, store nothing
     off[j] = static_cast<uint32_t>(s) * 16u;
@@ -206,19 +207,19 @@ __device__ __forceinline__ void reduce_scalar_cols(const Rows& rows,
   out[col] = a;
 }
 
-template <int U, int VPT, bool NT, class Rows>
-__global__ __launch_bounds__(kBlock) void k_reduce_vec(Rows rows,
+template <int BS, int U, int VPT, bool NT, class Rows>
+__global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
                                                        const float* __restrict__ w,
                                                        int64_t B, int64_t nvec,
                                                        int tail, const float* acc_in,
                                                        float* out, float W32,
                                                        int flags) {
-  const int64_t block_start = static_cast<int64_t>(blockIdx.x) * (kBlock * VPT);
-  const int64_t block_end = block_start + kBlock * VPT;
+  const int64_t block_start = static_cast<int64_t>(blockIdx.x) * (BS * VPT);
+  const int64_t block_end = block_start + BS * VPT;
   if (block_end <= nvec) {
-    reduce_vec_body<U, VPT, NT, false>(rows, w, B, nvec, acc_in, out, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, false>(rows, w, B, nvec, acc_in, out, W32, flags);
   } else if (block_start < nvec) {
-    reduce_vec_body<U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
   }
   // The last block also owns the (P % 4) scalar tail columns.
   if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
@@ -314,6 +315,31 @@ __global__ __launch_bounds__(kBlock) void k_adabest_sgd(const float* __restrict_
     adabest_elem(avg, beta, neg_lr, cloud, avg_prev, grad_out, i);
 }
 
+// FedDyn (feddyn.py:169-194): h += ratio * (cloud - avg); new = avg - h;
+// cloud <- fma(-lr, cloud - new, cloud); avg_prev <- avg.
+__global__ __launch_bounds__(kBlock) void k_feddyn_sgd(const float* __restrict__ avg,
+                                                       float ratio, float neg_lr,
+                                                       float* __restrict__ cloud,
+                                                       float* __restrict__ h,
+                                                       float* __restrict__ avg_prev,
+                                                       float* __restrict__ grad_out,
+                                                       int64_t P) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < P; i += stride) {
+    const float a = avg[i];
+    const float c = cloud[i];
+    const float g1 = c - a;
+    const float t = ratio * g1;
+    const float hn = h[i] + t;
+    const float nw = a - hn;
+    const float g = c - nw;
+    if (grad_out) grad_out[i] = g;
+    cloud[i] = sgd_rn(c, g, neg_lr);
+    h[i] = hn;
+    if (avg_prev) avg_prev[i] = a;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------
@@ -326,33 +352,44 @@ inline int elementwise_grid(int64_t n) {
   return static_cast<int>(g);
 }
 
-template <int U, int VPT, bool NT, class Rows>
+template <int BS, int U, int VPT, bool NT, class Rows>
 hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
                       const float* acc_in, float* out, float W32, int flags,
                       hipStream_t s) {
   const int64_t nvec = P / 4;
   const int tail = static_cast<int>(P - nvec * 4);
-  // one workgroup per kBlock*VPT float4 slots; the scalar tail belongs to the
+  // one workgroup per BS*VPT float4 slots; the scalar tail belongs to the
   // workgroup whose column span contains it (matters for RowsBlocked)
-  int64_t grid = (nvec + (tail > 0 ? 1 : 0) + kBlock * VPT - 1) / (kBlock * VPT);
+  int64_t grid = (nvec + (tail > 0 ? 1 : 0) + BS * VPT - 1) / (BS * VPT);
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_reduce_vec<U, VPT, NT, Rows>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kBlock), 0, s, rows, w, B, nvec, tail, acc_in, out, W32, flags);
+  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows>), dim3(static_cast<unsigned>(grid)),
+                     dim3(BS), 0, s, rows, w, B, nvec, tail, acc_in, out, W32, flags);
   return hipGetLastError();
 }
 
-template <int VPT, bool NT, class Rows>
+template <int BS, int VPT, bool NT, class Rows>
 hipError_t dispatch_unroll(int unroll_sel, const Rows& rows, const float* w, int64_t B,
                            int64_t P, const float* acc_in, float* out, float W32,
                            int flags, hipStream_t s) {
   switch (unroll_sel) {
-    case 1: return launch_vec<4, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
-    case 2: return launch_vec<8, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
-    case 3: return launch_vec<16, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
-    case 4: return launch_vec<2, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 1: return launch_vec<BS, 4, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 2: return launch_vec<BS, 8, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 3: return launch_vec<BS, 16, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 4: return launch_vec<BS, 2, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
     case 0:
-    default: return launch_vec<kDefaultUnroll, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    default:
+      return launch_vec<BS, kDefaultUnroll, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
   }
+}
+
+template <int BS, int VPT, class Rows>
+hipError_t dispatch_nt(const Rows& rows, const float* w, int64_t B, int64_t P,
+                       const float* acc_in, float* out, float W32, int flags, hipStream_t s) {
+  const int unroll_sel = (flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT;
+  return (flags & FEDAGG_NT)
+             ? dispatch_unroll<BS, VPT, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
+             : dispatch_unroll<BS, VPT, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags,
+                                               s);
 }
 
 template <class Rows>
@@ -366,20 +403,12 @@ hipError_t dispatch_reduce(const Rows& rows, bool vec_ok, const float* w, int64_
                        0, s, rows, w, B, P, acc_in, out, W32, flags);
     return hipGetLastError();
   }
-  const int unroll_sel = (flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT;
   const int vpt_sel = (flags & FEDAGG_VPT_MASK) >> FEDAGG_VPT_SHIFT;
-  const bool nt = (flags & FEDAGG_NT) != 0;
   switch (vpt_sel == 0 ? kDefaultVptSel : vpt_sel) {
-    case 1:
-      return nt ? dispatch_unroll<1, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-                : dispatch_unroll<1, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
-    case 3:
-      return nt ? dispatch_unroll<4, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-                : dispatch_unroll<4, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+    case 1: return dispatch_nt<kBlock, 1>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 3: return dispatch_nt<kBlock, 4>(rows, w, B, P, acc_in, out, W32, flags, s);
     case 2:
-    default:
-      return nt ? dispatch_unroll<2, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-                : dispatch_unroll<2, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
+    default: return dispatch_nt<kBlock, 2>(rows, w, B, P, acc_in, out, W32, flags, s);
   }
 }
 
@@ -392,7 +421,7 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (B > 0 && !w) return FEDAGG_EINVAL;
   if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
-                FEDAGG_VPT_MASK))
+                FEDAGG_VPT_MASK | FEDAGG_BS_MASK))
     return FEDAGG_EINVAL;
   return 0;
 }
@@ -450,25 +479,22 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   if (!aligned16(Xb) || !aligned16(out) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in)))
     return FEDAGG_EINVAL;
   RowsBlocked rows{Xb, Kcap, C};
-  const int unroll_sel = (flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT;
-  const bool nt = (flags & FEDAGG_NT) != 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // The column block is one workgroup's span: C = BS lanes * VPT slots * 4.
+  int bs_sel = (flags & FEDAGG_BS_MASK) >> FEDAGG_BS_SHIFT;
+  if (bs_sel == 0) bs_sel = kDefaultBsSel;
   hipError_t e;
-  switch (C) {  // the column block is one workgroup's span: C = 256 lanes * VPT * 4
-    case 1024:
-      e = nt ? dispatch_unroll<1, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-             : dispatch_unroll<1, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
-      break;
-    case 2048:
-      e = nt ? dispatch_unroll<2, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-             : dispatch_unroll<2, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
-      break;
-    case 4096:
-      e = nt ? dispatch_unroll<4, true>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s)
-             : dispatch_unroll<4, false>(unroll_sel, rows, w, B, P, acc_in, out, W32, flags, s);
-      break;
-    default:
-      return FEDAGG_EINVAL;
+  if (C == 1024) {
+    e = dispatch_nt<256, 1>(rows, w, B, P, acc_in, out, W32, flags, s);
+  } else if (C == 2048) {
+    e = bs_sel >= 2 ? dispatch_nt<512, 1>(rows, w, B, P, acc_in, out, W32, flags, s)
+                    : dispatch_nt<256, 2>(rows, w, B, P, acc_in, out, W32, flags, s);
+  } else if (C == 4096) {
+    e = bs_sel == 3   ? dispatch_nt<1024, 1>(rows, w, B, P, acc_in, out, W32, flags, s)
+        : bs_sel == 2 ? dispatch_nt<512, 2>(rows, w, B, P, acc_in, out, W32, flags, s)
+                      : dispatch_nt<256, 4>(rows, w, B, P, acc_in, out, W32, flags, s);
+  } else {
+    return FEDAGG_EINVAL;
   }
   return static_cast<int>(e);
 }
@@ -526,6 +552,17 @@ int fedagg_adabest_sgd_f32(const float* avg, float beta, float lr, float* cloud,
   if (!avg || !cloud || !avg_prev) return FEDAGG_EINVAL;
   hipLaunchKernelGGL(k_adabest_sgd, dim3(elementwise_grid(P)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), avg, beta, -lr, cloud, avg_prev,
+                     grad_out, P);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_feddyn_sgd_f32(const float* avg, float ratio, float lr, float* cloud, float* h,
+                          float* avg_prev, float* grad_out, int64_t P, void* stream) {
+  if (P < 0) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!avg || !cloud || !h) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_feddyn_sgd, dim3(elementwise_grid(P)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), avg, ratio, -lr, cloud, h, avg_prev,
                      grad_out, P);
   return static_cast<int>(hipGetLastError());
 }

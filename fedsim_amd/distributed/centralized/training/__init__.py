@@ -6,7 +6,8 @@ same names here.
 """
 from .adabest import AdaBest
 from .fedavg import FedAvg
+from .feddyn import FedDyn
 from .fednova import FedNova
 from .utils import serial_aggregation
 
-__all__ = ["FedAvg", "AdaBest", "FedNova", "serial_aggregation"]
+__all__ = ["FedAvg", "AdaBest", "FedNova", "FedDyn", "serial_aggregation"]

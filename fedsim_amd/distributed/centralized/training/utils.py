@@ -110,6 +110,30 @@ def fused_fedavg_step(cloud: torch.Tensor, avg: torch.Tensor, lr: float, optimiz
     _mark_stepped(optimizer)
 
 
+def _to_dev(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    """Working copy on ``dev`` (a fresh copy even if already there)."""
+    return t.detach().reshape(-1).to(dev, copy=True).contiguous()
+
+
+def fused_feddyn_step(cloud: torch.Tensor, avg: torch.Tensor, h: torch.Tensor, ratio: float,
+                      lr: float, optimizer):
+    """FedDyn epilogue in one kernel.  Returns (new_h, new_avg_params), each on
+    the device of the tensor it replaces."""
+    dev = _hip_device_for(avg, cloud)
+    c = cloud.data if cloud.device == dev else cloud.data.to(dev)
+    a = (avg if avg.device == dev else avg.to(dev)).reshape(-1)
+    hh = _to_dev(h, dev)
+    ap = torch.empty_like(c)
+    g = torch.empty_like(c)
+    ops.feddyn_sgd(a, c, hh, ratio, lr, avg_prev=ap, grad_out=g)
+    if c is not cloud.data:
+        cloud.data.copy_(c)
+    optimizer.zero_grad()
+    cloud.grad = g if g.device == cloud.device else g.to(cloud.device)
+    _mark_stepped(optimizer)
+    return hh.view_as(h).to(h.device), ap.view_as(cloud).to(cloud.device)
+
+
 def fused_adabest_step(cloud: torch.Tensor, avg: torch.Tensor, avg_prev: torch.Tensor,
                        beta: float, lr: float, optimizer) -> torch.Tensor:
     """h = beta*(avg_prev - avg); new = avg - h; cloud.grad = cloud - new;

@@ -39,12 +39,15 @@ def fl32(x) -> float:
     return float(np.float32(x))
 
 
-def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False) -> int:
+def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0) -> int:
+    """Kernel tuning bits (include/fedagg.h): k-unroll, float4 slots per lane
+    (row-major / pointer-table layouts), non-temporal loads, and the workgroup
+    size of the column-blocked layout.  0 = library default."""
     sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4}[unroll]
     vsel = {0: 0, 1: 1, 2: 2, 4: 3}[vpt]
-    return (sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT) | (
-        FEDAGG_NT if nt else 0
-    )
+    bsel = {0: 0, 256: 1, 512: 2, 1024: 3}[bs]
+    return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
+            | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0))
 
 
 # Tuned default for the column-blocked reduce (profiles/r01_sweep_*): k-unroll 4,
@@ -277,6 +280,27 @@ def fedavg_sgd(avg: torch.Tensor, cloud: torch.Tensor, lr: float,
         _stream_ptr(cloud.device),
     )
     check(rc, "fedagg_fedavg_sgd_f32")
+    return cloud
+
+
+def feddyn_sgd(avg: torch.Tensor, cloud: torch.Tensor, h: torch.Tensor, ratio: float,
+               lr: float, avg_prev: Optional[torch.Tensor] = None,
+               grad_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """In-place FedDyn server step (plain SGD): h += ratio*(cloud-avg); cloud
+    steps toward avg - h; ``avg_prev`` <- avg.  ``ratio`` is the Python float
+    weight / num_clients (rounded to fp32 here, as ATen does)."""
+    for t, n in ((avg, "avg"), (cloud, "cloud"), (h, "h")):
+        _require_hip_f32(t, n)
+        if t.numel() != cloud.numel():
+            raise ValueError(f"{n} size mismatch")
+    for t, n in ((avg_prev, "avg_prev"), (grad_out, "grad_out")):
+        if t is not None:
+            _require_hip_f32(t, n)
+    rc = _native.load().fedagg_feddyn_sgd_f32(
+        avg.data_ptr(), fl32(ratio), fl32(lr), cloud.data_ptr(), h.data_ptr(), _ptr(avg_prev),
+        _ptr(grad_out), cloud.numel(), _stream_ptr(cloud.device),
+    )
+    check(rc, "fedagg_feddyn_sgd_f32")
     return cloud
 
 

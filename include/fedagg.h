@@ -22,6 +22,9 @@
  *   fedagg_adabest_sgd_f32
  *       replaces AdaBest.optimize's h / new_params / pseudo-grad + SGD.step
  *       + avg_params write-back                    fedsim/distributed/centralized/training/adabest.py:178-188
+ *   fedagg_feddyn_sgd_f32
+ *       replaces FedDyn.optimize's h update, new_params, pseudo-grad + SGD.step
+ *                                                  fedsim/distributed/centralized/training/feddyn.py:169-194
  *
  * Bit-exactness contract (exact mode, the default): every output equals the
  * reference CPU aggregation bit for bit, given the same arrival order:
@@ -60,6 +63,10 @@ extern "C" {
 /* bits 12..13: float4 slots per lane, 0 = library default, 1 = 1, 2 = 2, 3 = 4 */
 #define FEDAGG_VPT_SHIFT 12
 #define FEDAGG_VPT_MASK  0x3000
+/* bits 14..15: workgroup size for the blocked layout, 0 = default, 1 = 256,
+ * 2 = 512, 3 = 1024 lanes (float4 slots per lane = C / (4 * lanes)) */
+#define FEDAGG_BS_SHIFT 14
+#define FEDAGG_BS_MASK  0xC000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
@@ -151,6 +158,19 @@ int fedagg_fedavg_sgd_f32(const float* avg, float lr, float* cloud,
 int fedagg_adabest_sgd_f32(const float* avg, float beta, float lr, float* cloud,
                            float* avg_prev, float* grad_out, int64_t P,
                            void* stream);
+
+/*
+ * FedDyn server step with plain SGD
+ * (fedsim/distributed/centralized/training/feddyn.py:169-194):
+ *   g1       = fl32(cloud - avg)
+ *   h'       = fl32(h + fl32(ratio32 * g1))      ratio32 = fl32(weight / num_clients)
+ *   new      = fl32(avg - h')
+ *   g        = fl32(cloud - new)
+ *   cloud'   = fma(-lr32, g, cloud)
+ *   avg_prev'= avg   (if avg_prev != NULL)
+ */
+int fedagg_feddyn_sgd_f32(const float* avg, float ratio, float lr, float* cloud, float* h,
+                          float* avg_prev, float* grad_out, int64_t P, void* stream);
 
 #ifdef __cplusplus
 }

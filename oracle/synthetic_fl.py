@@ -31,7 +31,8 @@ class FakeDataManager(object):
         return {}
 
     def get_oracle_dataset(self):
-        return None
+        # FedDyn.init reads len(oracle["train"]) / num_clients (feddyn.py:73-79)
+        return {"train": list(range(sum(self.sizes)))}
 
     def get_local_dataset(self, client_id):
         return {"train": list(range(self.sizes[client_id]))}

@@ -34,7 +34,7 @@ def _receive_all(algo_cls, case, agg, msgs, storage):
     from fedsim_amd.distributed.centralized.training import serial_aggregation
 
     for k, msg in enumerate(msgs):
-        if case["algo"] == "adabest":
+        if case["algo"] in ("adabest", "feddyn"):
             ok = serial_aggregation(storage, k, msg, "train", agg, train_weight=1)
         elif case["algo"] == "fednova":
             ok = serial_aggregation(storage, k, msg, "train", agg,
@@ -47,7 +47,7 @@ def _receive_all(algo_cls, case, agg, msgs, storage):
 @pytest.mark.parametrize("where", ["host", "device"])
 @pytest.mark.parametrize("case", FLOW_CASES, ids=[c["id"] for c in FLOW_CASES])
 def test_algorithm_round_bitwise(case, where, dev, golden):
-    from fedsim_amd.distributed.centralized.training import AdaBest, FedAvg
+    from fedsim_amd.distributed.centralized.training import AdaBest, FedAvg, FedDyn
     from fedsim_amd.utils import SerialAggregator, Storage
 
     _, arrays = golden
@@ -79,6 +79,15 @@ def test_algorithm_round_bitwise(case, where, dev, golden):
             ap = st.read("avg_params")
             assert ap.device == cloud_dev
             _expect(case, arrays, f"avg_params_lr{lr}", ap.cpu().numpy())
+        elif case["algo"] == "feddyn":
+            h0 = V.cloud_vector(case["P"], case["seed"] + 3)
+            st.write("h", torch.from_numpy(h0.copy()).to(cloud_dev))
+            st.write("num_clients", case["num_clients"])
+            reports = FedDyn.optimize(st, agg, None)
+            for name in ("h", "avg_params"):
+                t = st.read(name)
+                assert t.device == cloud_dev
+                _expect(case, arrays, f"{name}_lr{lr}", t.cpu().numpy())
         else:
             reports = FedAvg.optimize(st, agg, None)
         _expect(case, arrays, f"cloud_lr{lr}", cloud.detach().cpu().numpy())

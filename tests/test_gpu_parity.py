@@ -102,6 +102,12 @@ def test_epilogues_bitwise(case, dev, golden):
             prev = torch.from_numpy(V.cloud_vector(case["P"], case["seed"] + 2)).to(dev)
             ops.adabest_sgd(avg, cloud, prev, case["beta"], lr)
             _expect(case, arrays, f"avg_params_lr{lr}", prev.cpu().numpy())
+        elif case["algo"] == "feddyn":
+            h = torch.from_numpy(V.cloud_vector(case["P"], case["seed"] + 3)).to(dev)
+            ap = torch.empty_like(h)
+            ops.feddyn_sgd(avg, cloud, h, W / case["num_clients"], lr, avg_prev=ap)
+            _expect(case, arrays, f"h_lr{lr}", h.cpu().numpy())
+            _expect(case, arrays, f"avg_params_lr{lr}", ap.cpu().numpy())
         else:
             ops.fedavg_sgd(avg, cloud, lr)
         _expect(case, arrays, f"cloud_lr{lr}", cloud.cpu().numpy())

@@ -47,7 +47,10 @@ def test_round_loop_matches_reference(run, device, arrays):
     assert cloud.device.type == device
     np.testing.assert_array_equal(bits(cloud.detach().cpu().numpy()),
                                   bits(arrays[f"{run['id']}/cloud"]))
-    if run["algorithm"] == "AdaBest":
-        np.testing.assert_array_equal(bits(st.read("avg_params").cpu().numpy()),
-                                      bits(arrays[f"{run['id']}/avg_params"]))
+    for name in ("avg_params", "h"):
+        key = f"{run['id']}/{name}"
+        if key in arrays:
+            t = st.read(name)
+            assert t.device.type == device
+            np.testing.assert_array_equal(bits(t.detach().cpu().numpy()), bits(arrays[key]))
     assert {k: float(v) for k, v in scores.items()} == run["scores"]

@@ -34,6 +34,7 @@ RUNS = [
     ("FedAvg", dict(), dict(lr=0.3)),
     ("AdaBest", dict(mu=0.01, beta=0.6), dict(lr=1.0)),
     ("FedNova", dict(), dict(lr=0.7)),
+    ("FedDyn", dict(alpha=0.05), dict(lr=0.9)),
 ]
 
 
@@ -51,8 +52,10 @@ def run(R, name, alg_kwargs, opt_kwargs):
     scores = alg.train(rounds=S.ROUNDS)
     st = alg.get_server_storage()
     out = dict(cloud=st.read("cloud_params").detach().numpy().copy())
-    if name == "AdaBest":
+    if name in ("AdaBest", "FedDyn"):
         out["avg_params"] = st.read("avg_params").detach().numpy().copy()
+    if name == "FedDyn":
+        out["h"] = st.read("h").detach().numpy().copy()
     return out, {k: float(v) for k, v in scores.items()}
 
 
@@ -61,7 +64,7 @@ def main():
     import importlib
 
     tr = importlib.import_module("fedsim.distributed.centralized.training")
-    R = dict(FedAvg=tr.FedAvg, AdaBest=tr.AdaBest, FedNova=tr.FedNova)
+    R = dict(FedAvg=tr.FedAvg, AdaBest=tr.AdaBest, FedNova=tr.FedNova, FedDyn=tr.FedDyn)
     manifest, arrays = [], {}
     for i, (name, akw, okw) in enumerate(RUNS):
         out, scores = run(R, name, akw, okw)

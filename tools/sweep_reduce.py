@@ -49,15 +49,17 @@ def main():
     if a.blocked:
         C = a.blocked
         Xb = ops.to_blocked(Xv, C)
-        variants = [dict(unroll=u, vpt=C // 1024, nt=bool(n), table=False, blocked=C)
-                    for u, n in itertools.product((2, 4, 8), (0, 1))]
+        bss = {1024: (256,), 2048: (256, 512), 4096: (256, 512, 1024)}[C]
+        variants = [dict(unroll=u, bs=b, nt=bool(n), table=False, blocked=C)
+                    for u, n, b in itertools.product((2, 4, 8), (0, 1), bss)]
         del X, Xv, rows, table
         torch.cuda.empty_cache()
     alg = 4.0 * K * P + 4.0 * P
     times = {i: [] for i in range(len(variants))}
     for r in range(a.rounds):
         for i, var in enumerate(variants):
-            fl = ops.tuning_flags(unroll=var["unroll"], vpt=var["vpt"], nt=var["nt"])
+            fl = ops.tuning_flags(unroll=var["unroll"], vpt=var.get("vpt", 0), nt=var["nt"],
+                                  bs=var.get("bs", 0))
 
             def run():
                 if var.get("blocked"):
