@@ -315,6 +315,27 @@ __global__ __launch_bounds__(kBlock) void k_adabest_sgd(const float* __restrict_
     adabest_elem(avg, beta, neg_lr, cloud, avg_prev, grad_out, i);
 }
 
+// D2D pack of one client vector into row r of a column-blocked slab: a
+// streaming copy (16 B per lane in, 16 B per lane out, both coalesced inside a
+// column block).  The DMA engines are slower than the CUs for HBM->HBM copies.
+__global__ __launch_bounds__(kBlock) void k_pack_row(const float* __restrict__ src,
+                                                     int64_t P, float* __restrict__ Xb,
+                                                     int64_t Kcap, int64_t C, int64_t r) {
+  const int64_t nvec = P / 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t cvec = C / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec; i += stride) {
+    const int64_t b = i / cvec;
+    const int64_t c = i - b * cvec;
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src) + i);
+    reinterpret_cast<f32x4*>(Xb + (b * Kcap + r) * C)[c] = v;
+  }
+  if (blockIdx.x == 0 && static_cast<int64_t>(threadIdx.x) < P - nvec * 4) {
+    const int64_t p = nvec * 4 + threadIdx.x;
+    Xb[((p / C) * Kcap + r) * C + p % C] = src[p];
+  }
+}
+
 // FedDyn (feddyn.py:169-194): h += ratio * (cloud - avg); new = avg - h;
 // cloud <- fma(-lr, cloud - new, cloud); avg_prev <- avg.
 __global__ __launch_bounds__(kBlock) void k_feddyn_sgd(const float* __restrict__ avg,
@@ -506,6 +527,15 @@ int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, in
   if (P == 0) return 0;
   if (!src || !Xb) return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeDevice &&
+      aligned16(src) && aligned16(Xb)) {
+    // HBM -> HBM: copy kernel on the CUs
+    hipLaunchKernelGGL(k_pack_row, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0, s, src,
+                       P, Xb, Kcap, C, r);
+    return static_cast<int>(hipGetLastError());
+  }
+  (void)hipGetLastError();  // clear a failed attribute query on pageable memory
   const int64_t full = P / C;
   const int64_t rem = P - full * C;
   float* dst = Xb + r * C;

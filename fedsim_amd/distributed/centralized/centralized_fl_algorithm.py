@@ -87,7 +87,9 @@ class CentralFLAlgorithm(object):
         }
         oracle_dataset = data_manager.get_oracle_dataset()
 
-        self._aggregator_factory = aggregator_factory or SerialAggregator
+        # size each round's HBM ring once for the clients it will receive
+        self._aggregator_factory = aggregator_factory or partial(SerialAggregator,
+                                                                 expected_rows=sample_count)
         self._progress = progress
         self._server_memory = Storage()
         w = self._server_memory.write

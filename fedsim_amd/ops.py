@@ -50,9 +50,26 @@ def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0) -
             | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0))
 
 
-# Tuned default for the column-blocked reduce (profiles/r01_sweep_*): k-unroll 4,
-# non-temporal client-row loads; the float4 slots per lane follow from C.
+# Tuned defaults for the column-blocked reduce (profiles/r01_sweep*/: K=1000 at
+# P=25M and P=1.09M on MI355X): non-temporal client-row loads, 256-lane
+# workgroups; k-unroll 4 for C=4096, 2 for the narrower blocks.
 DEFAULT_FLAGS = tuning_flags(unroll=4, nt=True)
+_FLAGS_BY_C = {4096: tuning_flags(unroll=4, nt=True), 2048: tuning_flags(unroll=2, nt=True),
+               1024: tuning_flags(unroll=2, nt=True)}
+_MIN_WORKGROUPS = 2048  # ~8 per CU: below this, narrower column blocks win
+
+
+def choose_block_cols(P: int) -> int:
+    """Widest column block that still yields >= ~8 workgroups per CU (the
+    sweeps: C=4096 best at P=25M, C=1024 best at P=1.09M)."""
+    for C in (4096, 2048):
+        if (P + C - 1) // C >= _MIN_WORKGROUPS:
+            return C
+    return 1024
+
+
+def default_flags(C: int) -> int:
+    return _FLAGS_BY_C[C]
 
 
 def _stream_ptr(device: torch.device) -> int:

@@ -42,7 +42,6 @@ __all__ = ["SerialAggregator", "DeviceAggregator", "AppendixAggregator"]
 
 _DEFAULT_SLAB_BYTES = int(os.environ.get("FEDSIM_AMD_SLAB_BYTES", 16 << 30))
 _DEFAULT_MAX_ROWS = int(os.environ.get("FEDSIM_AMD_MAX_ROWS", 4096))
-_BLOCK_COLS = 4096  # columns per workgroup span in the blocked slab (sweep: fastest)
 _STAGING_SLOTS = 3
 
 
@@ -126,14 +125,14 @@ class _DeviceEntry(object):
         self.P = value.numel()
         self.out_device = value.device
         self.dev = dev
-        self.C = opts.block_cols
+        self.C = opts.block_cols or ops.choose_block_cols(self.P)
         self.nblk = (self.P + self.C - 1) // self.C
         row_bytes = 4 * max(1, self.nblk) * self.C
         self.Rmax = max(2, min(opts.max_rows, opts.slab_bytes // row_bytes))
         self.R = 0
         self.slab: Optional[torch.Tensor] = None
         self.hint = opts.expected_rows
-        self.flags = opts.flags
+        self.flags = ops.default_flags(self.C) if opts.flags is None else opts.flags
         self.agg = agg
         self.head = 0
         self.tail = 0
@@ -266,18 +265,18 @@ class SerialAggregator(object):
         slab_bytes: HBM budget of the pending-row ring per key; when it fills,
             pending rows are reduced into the accumulator (order is preserved).
         max_rows: cap on ring rows per key.
-        flags: libfedagg tuning flags (include/fedagg.h); default = tuned.
+        flags: libfedagg tuning flags (include/fedagg.h); default = tuned per C.
         expected_rows: hint (e.g. clients per round) to size the ring once.
-        block_cols: column-block width C of the slab (1024 / 2048 / 4096).
+        block_cols: column-block width C of the slab (1024 / 2048 / 4096);
+            default = ops.choose_block_cols(P).
     """
 
     def __init__(self, device=None, slab_bytes: int = _DEFAULT_SLAB_BYTES,
                  max_rows: int = _DEFAULT_MAX_ROWS, flags: Optional[int] = None,
-                 expected_rows: Optional[int] = None, block_cols: int = _BLOCK_COLS) -> None:
+                 expected_rows: Optional[int] = None,
+                 block_cols: Optional[int] = None) -> None:
         self._members: Dict = dict()
-        self._opts = _Options(device, slab_bytes, max_rows,
-                              ops.DEFAULT_FLAGS if flags is None else flags,
-                              expected_rows, block_cols)
+        self._opts = _Options(device, slab_bytes, max_rows, flags, expected_rows, block_cols)
         self._ingests: Dict = {}
 
     def _ingest(self, dev) -> _Ingest:

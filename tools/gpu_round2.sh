@@ -1,0 +1,17 @@
+#!/bin/bash
+# Tests + smoke + bench + per-config measurements + rocprof stats + ingest.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r01d}
+mkdir -p "$OUT"
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+&& timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+&& timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
+&& timeout -k 10 600 python tools/bench_configs.py > "$OUT/configs.jsonl" 2> "$OUT/configs.err" \
+&& timeout -k 10 300 python tools/bench_ingest.py > "$OUT/ingest.json" 2> "$OUT/ingest.err" \
+&& timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
+     -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.log" 2>&1
+rc=$?
+echo "exit $rc"
+exit $rc
