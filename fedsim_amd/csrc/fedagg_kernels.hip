@@ -362,6 +362,61 @@ __global__ __launch_bounds__(kBlock) void k_feddyn_sgd(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// General fused server step: algorithm pseudo-gradient + the full
+// torch.optim.SGD single-tensor update (torch/optim/sgd.py _single_tensor_sgd,
+// the path torch takes for CPU params), with every ATen op's rounding:
+//   d = maximize ? -g : g
+//   d = fma(param, wd, d)                         grad.add(param, alpha=wd)
+//   buf = first ? d : fma(d, 1-damp, fl(buf*m))   buf.mul_(m).add_(d, alpha=1-damp)
+//   d = nesterov ? fma(buf, m, d) : buf           grad.add(buf, alpha=m)
+//   param = fma(d, -lr, param)                    param.add_(d, alpha=-lr)
+// ---------------------------------------------------------------------------
+struct SgdArgs {
+  float neg_lr, momentum, one_minus_damp, wd;
+  int nesterov, maximize, first;
+};
+
+template <int ALGO, bool MOM>
+__global__ __launch_bounds__(kBlock) void k_server_step(const float* __restrict__ avg,
+                                                        float coef, float* __restrict__ cloud,
+                                                        float* __restrict__ aux,
+                                                        float* __restrict__ avg_prev,
+                                                        float* __restrict__ buf,
+                                                        float* __restrict__ grad_out,
+                                                        SgdArgs sa, int64_t P) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < P; i += stride) {
+    const float a = avg[i];
+    const float c = cloud[i];
+    float g;
+    if constexpr (ALGO == FEDAGG_ALGO_FEDAVG) {
+      g = c - a;  // fedavg.py:199
+    } else if constexpr (ALGO == FEDAGG_ALGO_ADABEST) {
+      const float h = coef * (aux[i] - a);  // adabest.py:178-180
+      const float nw = a - h;
+      g = c - nw;
+      aux[i] = a;  // avg_params <- avg (adabest.py:188)
+    } else {
+      const float g1 = c - a;  // feddyn.py:176-184
+      const float hn = aux[i] + coef * g1;
+      const float nw = a - hn;
+      g = c - nw;
+      aux[i] = hn;
+      if (avg_prev) avg_prev[i] = a;
+    }
+    if (grad_out) grad_out[i] = g;
+    float d = sa.maximize ? -g : g;
+    if (sa.wd != 0.f) d = __builtin_fmaf(c, sa.wd, d);
+    if constexpr (MOM) {
+      const float b = sa.first ? d : __builtin_fmaf(d, sa.one_minus_damp, buf[i] * sa.momentum);
+      buf[i] = b;
+      d = sa.nesterov ? __builtin_fmaf(b, sa.momentum, d) : b;
+    }
+    cloud[i] = __builtin_fmaf(d, sa.neg_lr, c);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -583,6 +638,38 @@ int fedagg_adabest_sgd_f32(const float* avg, float beta, float lr, float* cloud,
   hipLaunchKernelGGL(k_adabest_sgd, dim3(elementwise_grid(P)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), avg, beta, -lr, cloud, avg_prev,
                      grad_out, P);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_server_step_f32(int algo, const float* avg, float coef, float* cloud, float* aux,
+                           float* avg_prev, float* momentum_buf, int momentum_init,
+                           float* grad_out, const fedagg_sgd_params* sgd, int64_t P,
+                           void* stream) {
+  if (P < 0 || !sgd) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!avg || !cloud) return FEDAGG_EINVAL;
+  if (algo != FEDAGG_ALGO_FEDAVG && !aux) return FEDAGG_EINVAL;
+  const bool mom = sgd->momentum != 0.f;
+  if (mom && !momentum_buf) return FEDAGG_EINVAL;
+  if (sgd->nesterov && (!mom || sgd->one_minus_dampening != 1.f)) return FEDAGG_EINVAL;
+  SgdArgs sa{sgd->neg_lr, sgd->momentum, sgd->one_minus_dampening, sgd->weight_decay,
+             sgd->nesterov, sgd->maximize, momentum_init};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g(elementwise_grid(P)), b(kBlock);
+#define FEDAGG_STEP(A)                                                                    \
+  if (mom)                                                                                \
+    hipLaunchKernelGGL((k_server_step<A, true>), g, b, 0, s, avg, coef, cloud, aux,      \
+                       avg_prev, momentum_buf, grad_out, sa, P);                          \
+  else                                                                                    \
+    hipLaunchKernelGGL((k_server_step<A, false>), g, b, 0, s, avg, coef, cloud, aux,     \
+                       avg_prev, momentum_buf, grad_out, sa, P);
+  switch (algo) {
+    case FEDAGG_ALGO_FEDAVG: FEDAGG_STEP(FEDAGG_ALGO_FEDAVG) break;
+    case FEDAGG_ALGO_ADABEST: FEDAGG_STEP(FEDAGG_ALGO_ADABEST) break;
+    case FEDAGG_ALGO_FEDDYN: FEDAGG_STEP(FEDAGG_ALGO_FEDDYN) break;
+    default: return FEDAGG_EINVAL;
+  }
+#undef FEDAGG_STEP
   return static_cast<int>(hipGetLastError());
 }
 

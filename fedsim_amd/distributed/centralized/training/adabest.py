@@ -19,10 +19,6 @@ from .fedavg import FedAvg
 from .utils import fused_adabest_step, plain_sgd_lr, pop_average, serial_aggregation
 
 
-class _HostStats(SerialAggregator):
-    """Scalar-only running statistics (``avg_m``); never holds tensors."""
-
-
 class AdaBest(FedAvg):
     def init(server_storage, *args, **kwrag):
         default_mu = 0.1
@@ -34,7 +30,7 @@ class AdaBest(FedAvg):
         server_storage.write("average_sample", 0)
         server_storage.write("mu", kwrag.get("mu", default_mu))
         server_storage.write("beta", kwrag.get("beta", default_beta))
-        running_stats = _HostStats()
+        running_stats = SerialAggregator()  # scalar keys only: host arithmetic
         running_stats.add("avg_m", 0, 0)
         server_storage.write("running_stats", running_stats)
 

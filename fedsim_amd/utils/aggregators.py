@@ -40,7 +40,19 @@ from .dict_ops import apply_on_dict
 
 __all__ = ["SerialAggregator", "DeviceAggregator", "AppendixAggregator"]
 
-_DEFAULT_SLAB_BYTES = int(os.environ.get("FEDSIM_AMD_SLAB_BYTES", 16 << 30))
+_ENV_SLAB_BYTES = os.environ.get("FEDSIM_AMD_SLAB_BYTES")
+_DEFAULT_SLAB_BYTES = int(_ENV_SLAB_BYTES) if _ENV_SLAB_BYTES else None
+_SLAB_CAP = 64 << 30  # per key; a quarter of HBM at most (288 GB on MI355X)
+
+
+def _slab_budget(dev: torch.device, requested: Optional[int]) -> int:
+    """HBM budget of one key's ring.  Each drain re-reads and re-writes the
+    4P-byte accumulator, so a long ring keeps that overhead at ~1 % (SURVEY
+    §8d): default min(64 GiB, total HBM / 4)."""
+    if requested is not None:
+        return requested
+    total = torch.cuda.get_device_properties(dev).total_memory
+    return min(_SLAB_CAP, total // 4)
 _DEFAULT_MAX_ROWS = int(os.environ.get("FEDSIM_AMD_MAX_ROWS", 4096))
 _STAGING_SLOTS = 3
 
@@ -128,7 +140,7 @@ class _DeviceEntry(object):
         self.C = opts.block_cols or ops.choose_block_cols(self.P)
         self.nblk = (self.P + self.C - 1) // self.C
         row_bytes = 4 * max(1, self.nblk) * self.C
-        self.Rmax = max(2, min(opts.max_rows, opts.slab_bytes // row_bytes))
+        self.Rmax = max(2, min(opts.max_rows, _slab_budget(dev, opts.slab_bytes) // row_bytes))
         self.R = 0
         self.slab: Optional[torch.Tensor] = None
         self.hint = opts.expected_rows
@@ -271,7 +283,7 @@ class SerialAggregator(object):
             default = ops.choose_block_cols(P).
     """
 
-    def __init__(self, device=None, slab_bytes: int = _DEFAULT_SLAB_BYTES,
+    def __init__(self, device=None, slab_bytes: Optional[int] = _DEFAULT_SLAB_BYTES,
                  max_rows: int = _DEFAULT_MAX_ROWS, flags: Optional[int] = None,
                  expected_rows: Optional[int] = None,
                  block_cols: Optional[int] = None) -> None:

@@ -25,6 +25,9 @@
  *   fedagg_feddyn_sgd_f32
  *       replaces FedDyn.optimize's h update, new_params, pseudo-grad + SGD.step
  *                                                  fedsim/distributed/centralized/training/feddyn.py:169-194
+ *   fedagg_server_step_f32
+ *       the three optimize epilogues above with any torch.optim.SGD
+ *       configuration (momentum / nesterov / weight decay / maximize)
  *
  * Bit-exactness contract (exact mode, the default): every output equals the
  * reference CPU aggregation bit for bit, given the same arrival order:
@@ -171,6 +174,46 @@ int fedagg_adabest_sgd_f32(const float* avg, float beta, float lr, float* cloud,
  */
 int fedagg_feddyn_sgd_f32(const float* avg, float ratio, float lr, float* cloud, float* h,
                           float* avg_prev, float* grad_out, int64_t P, void* stream);
+
+/*
+ * General fused server step: an algorithm's pseudo-gradient followed by the
+ * full torch.optim.SGD update (momentum, dampening, nesterov, weight decay,
+ * maximize) with ATen's roundings (torch/optim/sgd.py _single_tensor_sgd, the
+ * path torch takes for CPU params):
+ *   d   = maximize ? -g : g
+ *   d   = fma(param, wd, d)                          if wd != 0
+ *   buf = init ? d : fma(d, 1-damp, fl32(buf * m))   if m != 0
+ *   d   = nesterov ? fma(buf, m, d) : buf            if m != 0
+ *   param = fma(d, -lr, param)
+ * g per algo:
+ *   FEDAGG_ALGO_FEDAVG   g = cloud - avg                        (fedavg.py:199)
+ *   FEDAGG_ALGO_ADABEST  g = cloud - (avg - coef*(aux - avg)),  aux <- avg
+ *                        coef = beta, aux = avg_params          (adabest.py:178-188)
+ *   FEDAGG_ALGO_FEDDYN   aux <- aux + coef*(cloud - avg); g = cloud - (avg - aux);
+ *                        avg_prev <- avg (if non-NULL)
+ *                        coef = weight/num_clients, aux = h     (feddyn.py:176-192)
+ * The scalars in *sgd are the fp32 values ATen computes with: each is the
+ * Python double rounded once (neg_lr = fl32(-lr), one_minus_dampening =
+ * fl32(1 - dampening)).  momentum_init != 0 means the optimizer has no
+ * momentum buffer yet (torch clones d into it).  grad_out receives g.
+ */
+#define FEDAGG_ALGO_FEDAVG  0
+#define FEDAGG_ALGO_ADABEST 1
+#define FEDAGG_ALGO_FEDDYN  2
+
+typedef struct fedagg_sgd_params {
+  float neg_lr;
+  float momentum;
+  float one_minus_dampening;
+  float weight_decay;
+  int nesterov;
+  int maximize;
+} fedagg_sgd_params;
+
+int fedagg_server_step_f32(int algo, const float* avg, float coef, float* cloud, float* aux,
+                           float* avg_prev, float* momentum_buf, int momentum_init,
+                           float* grad_out, const fedagg_sgd_params* sgd, int64_t P,
+                           void* stream);
 
 #ifdef __cplusplus
 }

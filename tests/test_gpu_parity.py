@@ -184,3 +184,16 @@ def test_pack_row_layout(dev):
         torch.cuda.synchronize()
         ref_b = ops.to_blocked(X.to(dev), C)
         assert torch.equal(Xb, ref_b)
+        # HBM -> HBM pack (copy kernel) and unaligned device source (DMA path)
+        Xb2 = torch.zeros_like(Xb)
+        Xd = X.to(dev)
+        for k in range(K):
+            ops.pack_row(Xd[k].contiguous(), Xb2, k)
+        assert torch.equal(Xb2, ref_b)
+        if P > 1:
+            Xu = torch.zeros(K, P + 1, device=dev)
+            Xu[:, 1:] = Xd
+            Xb3 = torch.zeros(ops.blocked_shape(K, P, C), device=dev)
+            for k in range(K):
+                ops.pack_row(Xu[k, 1:], Xb3, k)  # 4-byte aligned source
+            assert torch.equal(Xb3, ref_b)

@@ -119,7 +119,7 @@ def main():
         torch.cuda.empty_cache()
 
     if "cfg5" in only:
-        K, P, pool = 12_500, 125_000_000, 50
+        K, P, pool = 12_500, 125_000_000, 100
         passes = K // pool
         Xb = blocked_random(pool, P, dev, 3 + rank)
         ws = [int(v) for v in rng.integers(50, 601, size=pool)]
@@ -138,7 +138,7 @@ def main():
         if dist is not None:
             dist.barrier()
         report("cfg5_client_shard_allreduce", K, P, timed(fn, max(1, a.steps // 2), warmup=1),
-               dict(pool_rows=pool, note="K_per_gpu streamed from a resident 25 GB pool; "
+               dict(pool_rows=pool, note="K_per_gpu streamed from a resident 50 GB pool; "
                                          "RCCL all-reduce of 4P bytes when N>1"))
         del Xb
 
