@@ -31,10 +31,28 @@ FEDAGG_SCALAR = 0x8
 FEDAGG_UNROLL_SHIFT = 8
 FEDAGG_VPT_SHIFT = 12
 FEDAGG_BS_SHIFT = 14
+FEDAGG_FLAT = 0x10000
 FEDAGG_EINVAL = -22
 
+FEDAGG_ALGO_FEDAVG = 0
+FEDAGG_ALGO_ADABEST = 1
+FEDAGG_ALGO_FEDDYN = 2
+
+
+class SgdParams(ctypes.Structure):
+    """struct fedagg_sgd_params (include/fedagg.h)."""
+
+    _fields_ = [
+        ("neg_lr", ctypes.c_float),
+        ("momentum", ctypes.c_float),
+        ("one_minus_dampening", ctypes.c_float),
+        ("weight_decay", ctypes.c_float),
+        ("nesterov", ctypes.c_int),
+        ("maximize", ctypes.c_int),
+    ]
+
+
 # (name, restype, argtypes) for every symbol include/fedagg.h declares.
-_c_float_p = ctypes.c_void_p
 SIGNATURES = {
     "fedagg_abi_version": (ctypes.c_int, []),
     "fedagg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -75,6 +93,12 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p],
+    ),
+    "fedagg_server_step_f32": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+         ctypes.POINTER(SgdParams), ctypes.c_int64, ctypes.c_void_p],
     ),
     "fedagg_feddyn_sgd_f32": (
         ctypes.c_int,

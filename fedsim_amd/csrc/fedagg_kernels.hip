@@ -49,6 +49,7 @@ constexpr int kDefaultBsSel = 1;   // blocked layout: 256-lane workgroups
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).
 using f32x4 = float __attribute__((ext_vector_type(4)));
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // Row addressing policies
@@ -59,6 +60,8 @@ struct RowsStrided {
   __device__ __forceinline__ const char* row(int64_t k) const {
     return reinterpret_cast<const char*>(X + k * ldx);
   }
+  template <bool NT>
+  __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const;
 };
 
 // Column-blocked slab: for column block b (C floats = one workgroup's span),
@@ -74,6 +77,36 @@ struct RowsBlocked {
     return reinterpret_cast<const char*>(
         X + (static_cast<int64_t>(blockIdx.x) * (Kcap - 1) + k) * C);
   }
+  template <bool NT>
+  __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const;
+};
+
+// Same layout, loaded with buffer instructions: the workgroup's region is one
+// buffer descriptor (SGPRs), the row is an SGPR soffset (k * C * 4) and the
+// lane's column is a 32-bit VGPR voffset, so every load is
+//   buffer_load_dwordx4 v, v_off, s[rsrc], s_row offen [nt]
+// and the unrolled loop needs one VGPR per column slot for addressing instead
+// of a 64-bit VGPR pointer per in-flight load (134 -> ~90 VGPRs at U=4, VPT=4).
+struct RowsBlockedBuf {
+  const float* X;
+  int64_t Kcap;
+  int64_t C;
+  __device__ __forceinline__ const char* row(int64_t k) const {
+    return reinterpret_cast<const char*>(
+        X + (static_cast<int64_t>(blockIdx.x) * (Kcap - 1) + k) * C);
+  }
+  template <bool NT>
+  __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const {
+    const char* region = reinterpret_cast<const char*>(X + static_cast<int64_t>(blockIdx.x) * Kcap * C);
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(region), static_cast<short>(0),
+        static_cast<int>(static_cast<uint32_t>(Kcap * C * 4)), 0x00020000);
+    const uint32_t voff = goff - static_cast<uint32_t>(blockIdx.x) * static_cast<uint32_t>(C * 4);
+    const uint32_t soff = static_cast<uint32_t>(k) * static_cast<uint32_t>(C * 4);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(voff),
+                                                          static_cast<int>(soff), NT ? 2 : 0);
+    return __builtin_bit_cast(f32x4, v);
+  }
 };
 
 struct RowsTable {
@@ -81,6 +114,8 @@ struct RowsTable {
   __device__ __forceinline__ const char* row(int64_t k) const {
     return reinterpret_cast<const char*>(rows[k]);
   }
+  template <bool NT>
+  __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const;
 };
 
 template <bool NT>
@@ -91,6 +126,19 @@ __device__ __forceinline__ f32x4 ld4(const char* base, uint32_t off) {
   } else {
     return *p;
   }
+}
+
+template <bool NT>
+__device__ __forceinline__ f32x4 RowsStrided::load4(int64_t k, uint32_t goff) const {
+  return ld4<NT>(row(k), goff);
+}
+template <bool NT>
+__device__ __forceinline__ f32x4 RowsBlocked::load4(int64_t k, uint32_t goff) const {
+  return ld4<NT>(row(k), goff);
+}
+template <bool NT>
+__device__ __forceinline__ f32x4 RowsTable::load4(int64_t k, uint32_t goff) const {
+  return ld4<NT>(row(k), goff);
 }
 
 template <bool NT>
@@ -165,9 +213,8 @@ __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
     f32x4 v[U][VPT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const char* r = rows.row(k + u);
 #pragma unroll
-      for (int j = 0; j < VPT; ++j) v[u][j] = ld4<NT>(r, off[j]);
+      for (int j = 0; j < VPT; ++j) v[u][j] = rows.template load4<NT>(k + u, off[j]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -177,10 +224,9 @@ __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
     }
   }
   for (; k < B; ++k) {
-    const char* r = rows.row(k);
     const float wk = w[k];
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], ld4<NT>(r, off[j]), wk);
+    for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], rows.template load4<NT>(k, off[j]), wk);
   }
 
   if (flags & FEDAGG_FINALIZE) {
@@ -488,6 +534,22 @@ hipError_t dispatch_reduce(const Rows& rows, bool vec_ok, const float* w, int64_
   }
 }
 
+// The column block is one workgroup's span: C = BS lanes * VPT slots * 4.
+template <class Rows>
+hipError_t dispatch_blocked(const Rows& rows, int64_t C, int bs_sel, const float* w, int64_t B,
+                            int64_t P, const float* acc_in, float* out, float W32, int flags,
+                            hipStream_t s) {
+  if (C == 1024) return dispatch_nt<256, 1>(rows, w, B, P, acc_in, out, W32, flags, s);
+  if (C == 2048)
+    return bs_sel >= 2 ? dispatch_nt<512, 1>(rows, w, B, P, acc_in, out, W32, flags, s)
+                       : dispatch_nt<256, 2>(rows, w, B, P, acc_in, out, W32, flags, s);
+  if (C == 4096)
+    return bs_sel == 3   ? dispatch_nt<1024, 1>(rows, w, B, P, acc_in, out, W32, flags, s)
+           : bs_sel == 2 ? dispatch_nt<512, 2>(rows, w, B, P, acc_in, out, W32, flags, s)
+                         : dispatch_nt<256, 4>(rows, w, B, P, acc_in, out, W32, flags, s);
+  return hipErrorInvalidValue;
+}
+
 int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
                       const float* out, int flags) {
   if (B < 0 || P < 0) return FEDAGG_EINVAL;
@@ -497,7 +559,7 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (B > 0 && !w) return FEDAGG_EINVAL;
   if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
-                FEDAGG_VPT_MASK | FEDAGG_BS_MASK))
+                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT))
     return FEDAGG_EINVAL;
   return 0;
 }
@@ -554,24 +616,19 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   if (B > Kcap || (B > 0 && !Xb)) return FEDAGG_EINVAL;
   if (!aligned16(Xb) || !aligned16(out) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in)))
     return FEDAGG_EINVAL;
-  RowsBlocked rows{Xb, Kcap, C};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // The column block is one workgroup's span: C = BS lanes * VPT slots * 4.
   int bs_sel = (flags & FEDAGG_BS_MASK) >> FEDAGG_BS_SHIFT;
   if (bs_sel == 0) bs_sel = kDefaultBsSel;
   hipError_t e;
-  if (C == 1024) {
-    e = dispatch_nt<256, 1>(rows, w, B, P, acc_in, out, W32, flags, s);
-  } else if (C == 2048) {
-    e = bs_sel >= 2 ? dispatch_nt<512, 1>(rows, w, B, P, acc_in, out, W32, flags, s)
-                    : dispatch_nt<256, 2>(rows, w, B, P, acc_in, out, W32, flags, s);
-  } else if (C == 4096) {
-    e = bs_sel == 3   ? dispatch_nt<1024, 1>(rows, w, B, P, acc_in, out, W32, flags, s)
-        : bs_sel == 2 ? dispatch_nt<512, 2>(rows, w, B, P, acc_in, out, W32, flags, s)
-                      : dispatch_nt<256, 4>(rows, w, B, P, acc_in, out, W32, flags, s);
+  // buffer-descriptor path unless asked for flat loads or a block region is
+  // too large for a 32-bit descriptor range
+  if ((flags & FEDAGG_FLAT) || Kcap * C * 4 >= (int64_t(1) << 32)) {
+    e = dispatch_blocked(RowsBlocked{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags, s);
   } else {
-    return FEDAGG_EINVAL;
+    e = dispatch_blocked(RowsBlockedBuf{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags,
+                         s);
   }
+  if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
   return static_cast<int>(e);
 }
 

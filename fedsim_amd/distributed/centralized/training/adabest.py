@@ -16,7 +16,7 @@ import torch
 from ....local import default_step_closure
 from ....utils import SerialAggregator, vector_to_parameters_like, vectorize_module
 from .fedavg import FedAvg
-from .utils import fused_adabest_step, plain_sgd_lr, pop_average, serial_aggregation
+from .utils import fused_server_step, pop_average, serial_aggregation, sgd_config
 
 
 class AdaBest(FedAvg):
@@ -91,10 +91,10 @@ class AdaBest(FedAvg):
             lr_scheduler = server_storage.read("lr_scheduler")
             cloud_params = server_storage.read("cloud_params")
             avg_params = server_storage.read("avg_params")
-            lr = plain_sgd_lr(optimizer, cloud_params)
-            if lr is not None:
-                new_avg = fused_adabest_step(cloud_params, param_avg, avg_params, beta, lr,
-                                             optimizer)
+            cfg = sgd_config(optimizer, cloud_params)
+            if cfg is not None:
+                new_avg, _ = fused_server_step("adabest", cloud_params, param_avg, optimizer,
+                                               cfg, coef=beta, aux=avg_params)
             else:
                 param_avg = param_avg.to(cloud_params.device)
                 h = beta * (avg_params - param_avg)

@@ -8,8 +8,8 @@ Plugin surface identical to the reference
 On the accelerated path:
   receive_from_client -> serial_aggregation -> SerialAggregator.add
       (client vector snapshotted into HBM; reduced by libfedagg)
-  optimize            -> pop (fused reduce + divide) + fused SGD epilogue
-      (fedavg.py:193-208; bit-identical to torch CPU)
+  optimize            -> pop (fused reduce + divide) + fused pseudo-grad / SGD
+      step, any SGD configuration (fedavg.py:193-208; bit-identical to torch CPU)
 """
 from __future__ import annotations
 
@@ -20,7 +20,7 @@ from torch.utils.data import DataLoader, RandomSampler
 from ....local import default_step_closure, local_inference, local_train
 from ....utils import initialize_module, vectorize_module
 from ..centralized_fl_algorithm import CentralFLAlgorithm
-from .utils import fused_fedavg_step, plain_sgd_lr, pop_average, serial_aggregation
+from .utils import fused_server_step, pop_average, serial_aggregation, sgd_config
 
 
 class FedAvg(CentralFLAlgorithm):
@@ -88,9 +88,9 @@ class FedAvg(CentralFLAlgorithm):
             optimizer = server_storage.read("optimizer")
             lr_scheduler = server_storage.read("lr_scheduler")
             cloud_params = server_storage.read("cloud_params")
-            lr = plain_sgd_lr(optimizer, cloud_params)
-            if lr is not None:
-                fused_fedavg_step(cloud_params, param_avg, lr, optimizer)
+            cfg = sgd_config(optimizer, cloud_params)
+            if cfg is not None:
+                fused_server_step("fedavg", cloud_params, param_avg, optimizer, cfg)
             else:
                 pseudo_grads = cloud_params.data - param_avg.to(cloud_params.device)
                 optimizer.zero_grad()

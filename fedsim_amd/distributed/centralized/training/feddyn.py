@@ -16,7 +16,7 @@ import torch
 from ....local import default_step_closure
 from ....utils import vector_to_parameters_like, vectorize_module
 from .fedavg import FedAvg
-from .utils import fused_feddyn_step, plain_sgd_lr, pop_average, serial_aggregation
+from .utils import fused_server_step, pop_average, serial_aggregation, sgd_config
 
 
 class FedDyn(FedAvg):
@@ -83,10 +83,11 @@ class FedDyn(FedAvg):
             h = server_storage.read("h")
             num_clients = server_storage.read("num_clients")
             server_storage.change_protection("num_clients", False, False)
-            lr = plain_sgd_lr(optimizer, cloud_params)
-            if lr is not None:
-                h, new_avg = fused_feddyn_step(cloud_params, param_avg, h,
-                                               weight / num_clients, lr, optimizer)
+            cfg = sgd_config(optimizer, cloud_params)
+            if cfg is not None:
+                h, new_avg = fused_server_step("feddyn", cloud_params, param_avg, optimizer,
+                                               cfg, coef=weight / num_clients, aux=h,
+                                               want_avg_prev=True)
             else:
                 param_avg = param_avg.to(cloud_params.device)
                 pseudo_grads = cloud_params.data - param_avg

@@ -1,4 +1,4 @@
-"""serial_aggregation and the fused server-step helpers.
+"""serial_aggregation and the fused server step.
 
 ``serial_aggregation`` keeps the reference contract
 (fedsim/distributed/centralized/training/utils.py:7-57): divergence -> False,
@@ -7,12 +7,14 @@ weight is <= 0, per-split scalar metrics added with the (sticky) other_weight.
 The reference's defensive ``clone()`` (utils.py:34) is dropped: the aggregator's
 ``add`` already snapshots the vector into HBM, so the copy bought nothing.
 
-The server-step helpers run the FedAvg / AdaBest epilogues
-(fedavg.py:193-208, adabest.py:172-189) as one fused libfedagg kernel when the
-server optimizer is plain SGD, reproducing torch CPU SGD.step bit for bit
-(``param.add_(grad, alpha=-lr)`` = fma(-lr, g, p), torch/optim/sgd.py).
-Any other optimizer takes the reference's torch.optim route on the averaged
-vector (the aggregation itself is still the HIP kernel).
+``fused_server_step`` runs the FedAvg / AdaBest / FedDyn ``optimize`` epilogues
+(fedavg.py:193-208, adabest.py:172-189, feddyn.py:169-194) together with the
+server optimizer's update as ONE libfedagg kernel whenever the optimizer is a
+``torch.optim.SGD`` over exactly ``[cloud_params]`` (any momentum / dampening /
+nesterov / weight decay / maximize).  It reproduces torch CPU SGD.step bit for
+bit, including the momentum buffer it leaves in ``optimizer.state``.  Any other
+optimizer takes the reference's torch.optim route on the averaged vector (the
+aggregation itself is still the HIP kernel).
 """
 from __future__ import annotations
 
@@ -65,22 +67,38 @@ def pop_average(aggregator, key="local_params") -> torch.Tensor:
     return aggregator.pop(key)
 
 
-def plain_sgd_lr(optimizer, param) -> Optional[float]:
-    """lr if ``optimizer`` is torch.optim.SGD over exactly ``[param]`` with no
-    momentum / weight decay / nesterov / maximize, else None."""
+def _scalar(x) -> Optional[float]:
+    if isinstance(x, torch.Tensor):
+        return float(x.item()) if x.numel() == 1 else None
+    return float(x)
+
+
+def sgd_config(optimizer, param) -> Optional[dict]:
+    """The SGD hyper-parameters if ``optimizer`` is torch.optim.SGD over
+    exactly ``[param]`` (fp32, contiguous), else None."""
     if type(optimizer) is not torch.optim.SGD or len(optimizer.param_groups) != 1:
         return None
     g = optimizer.param_groups[0]
     if len(g["params"]) != 1 or g["params"][0] is not param:
         return None
-    if g.get("momentum", 0) or g.get("weight_decay", 0) or g.get("nesterov", False) or g.get(
-        "maximize", False
-    ):
-        return None
     if param.dtype != torch.float32 or not param.is_contiguous():
         return None
-    lr = g["lr"]
-    return float(lr.item()) if isinstance(lr, torch.Tensor) else float(lr)
+    cfg = dict(lr=_scalar(g["lr"]), momentum=_scalar(g.get("momentum", 0)),
+               dampening=_scalar(g.get("dampening", 0)),
+               weight_decay=_scalar(g.get("weight_decay", 0)),
+               nesterov=bool(g.get("nesterov", False)), maximize=bool(g.get("maximize", False)))
+    if any(v is None for v in cfg.values()):
+        return None
+    return cfg
+
+
+def plain_sgd_lr(optimizer, param) -> Optional[float]:
+    """lr if ``optimizer`` is a momentum-free, decay-free SGD over ``[param]``."""
+    cfg = sgd_config(optimizer, param)
+    if cfg is None or cfg["momentum"] or cfg["weight_decay"] or cfg["nesterov"] or \
+            cfg["maximize"]:
+        return None
+    return cfg["lr"]
 
 
 def _hip_device_for(*tensors) -> torch.device:
@@ -90,65 +108,45 @@ def _hip_device_for(*tensors) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def _mark_stepped(optimizer) -> None:
-    # The fused kernel replaces optimizer.step(); tell LR schedulers a step
-    # happened (torch/optim/lr_scheduler.py checks optimizer._opt_called).
-    optimizer._opt_called = True
-
-
-def fused_fedavg_step(cloud: torch.Tensor, avg: torch.Tensor, lr: float, optimizer) -> None:
-    """cloud.grad = cloud - avg ; cloud <- fma(-lr, grad, cloud), one kernel."""
-    dev = _hip_device_for(avg, cloud)
-    c = cloud.data if cloud.device == dev else cloud.data.to(dev)
-    a = (avg if avg.device == dev else avg.to(dev)).reshape(-1)
-    g = torch.empty_like(c)
-    ops.fedavg_sgd(a, c, lr, grad_out=g)
-    if c is not cloud.data:
-        cloud.data.copy_(c)
-    optimizer.zero_grad()
-    cloud.grad = g if g.device == cloud.device else g.to(cloud.device)
-    _mark_stepped(optimizer)
-
-
-def _to_dev(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
-    """Working copy on ``dev`` (a fresh copy even if already there)."""
+def _work_copy(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    """Flat contiguous copy on ``dev`` (always a fresh copy)."""
     return t.detach().reshape(-1).to(dev, copy=True).contiguous()
 
 
-def fused_feddyn_step(cloud: torch.Tensor, avg: torch.Tensor, h: torch.Tensor, ratio: float,
-                      lr: float, optimizer):
-    """FedDyn epilogue in one kernel.  Returns (new_h, new_avg_params), each on
-    the device of the tensor it replaces."""
+def fused_server_step(algo: str, cloud: torch.Tensor, avg: torch.Tensor, optimizer,
+                      cfg: dict, coef: float = 0.0, aux: Optional[torch.Tensor] = None,
+                      want_avg_prev: bool = False):
+    """One kernel: algorithm pseudo-gradient + SGD update of ``cloud``.
+
+    Leaves ``cloud.grad`` = pseudo-gradient and the momentum buffer in
+    ``optimizer.state[cloud]`` exactly as ``optimizer.step()`` would, and marks
+    the optimizer as stepped for LR schedulers.  Returns ``(aux', avg_prev')``
+    on the devices of ``aux`` / ``cloud`` (None where not requested)."""
     dev = _hip_device_for(avg, cloud)
     c = cloud.data if cloud.device == dev else cloud.data.to(dev)
-    a = (avg if avg.device == dev else avg.to(dev)).reshape(-1)
-    hh = _to_dev(h, dev)
-    ap = torch.empty_like(c)
+    a = (avg if avg.device == dev else avg.to(dev)).reshape(-1).contiguous()
+    x = _work_copy(aux, dev) if aux is not None else None
+    ap = torch.empty_like(c) if want_avg_prev else None
     g = torch.empty_like(c)
-    ops.feddyn_sgd(a, c, hh, ratio, lr, avg_prev=ap, grad_out=g)
+    state = optimizer.state[cloud]
+    buf, init = None, False
+    if cfg["momentum"] != 0:
+        prev = state.get("momentum_buffer")
+        init = prev is None
+        buf = torch.empty_like(c) if init else _work_copy(prev, dev)
+    ops.server_step(algo, a, c, lr=cfg["lr"], momentum=cfg["momentum"],
+                    dampening=cfg["dampening"], weight_decay=cfg["weight_decay"],
+                    nesterov=cfg["nesterov"], maximize=cfg["maximize"], coef=coef, aux=x,
+                    avg_prev=ap, momentum_buf=buf, momentum_init=init, grad_out=g)
     if c is not cloud.data:
         cloud.data.copy_(c)
     optimizer.zero_grad()
     cloud.grad = g if g.device == cloud.device else g.to(cloud.device)
-    _mark_stepped(optimizer)
-    return hh.view_as(h).to(h.device), ap.view_as(cloud).to(cloud.device)
-
-
-def fused_adabest_step(cloud: torch.Tensor, avg: torch.Tensor, avg_prev: torch.Tensor,
-                       beta: float, lr: float, optimizer) -> torch.Tensor:
-    """h = beta*(avg_prev - avg); new = avg - h; cloud.grad = cloud - new;
-    cloud <- fma(-lr, grad, cloud); avg_prev <- avg.  Returns the new
-    avg_params tensor (on avg_prev's device)."""
-    dev = _hip_device_for(avg, cloud)
-    c = cloud.data if cloud.device == dev else cloud.data.to(dev)
-    a = (avg if avg.device == dev else avg.to(dev)).reshape(-1)
-    ap = avg_prev.detach().clone() if avg_prev.device == dev else avg_prev.to(dev)
-    ap = ap.reshape(-1).contiguous()
-    g = torch.empty_like(c)
-    ops.adabest_sgd(a, c, ap, beta, lr, grad_out=g)
-    if c is not cloud.data:
-        cloud.data.copy_(c)
-    optimizer.zero_grad()
-    cloud.grad = g if g.device == cloud.device else g.to(cloud.device)
-    _mark_stepped(optimizer)
-    return ap.view_as(avg_prev) if ap.device == avg_prev.device else ap.to(avg_prev.device)
+    if buf is not None:
+        state["momentum_buffer"] = buf.view_as(cloud).to(cloud.device)
+    # The kernel replaced optimizer.step(); LR schedulers check this flag
+    # (torch/optim/lr_scheduler.py) to detect a step.
+    optimizer._opt_called = True
+    x_out = None if x is None else x.view_as(aux).to(aux.device)
+    ap_out = None if ap is None else ap.view_as(cloud).to(cloud.device)
+    return x_out, ap_out

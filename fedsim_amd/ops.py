@@ -39,15 +39,18 @@ def fl32(x) -> float:
     return float(np.float32(x))
 
 
-def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0) -> int:
+def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
+                 flat: bool = False) -> int:
     """Kernel tuning bits (include/fedagg.h): k-unroll, float4 slots per lane
-    (row-major / pointer-table layouts), non-temporal loads, and the workgroup
-    size of the column-blocked layout.  0 = library default."""
+    (row-major / pointer-table layouts), non-temporal loads, the workgroup
+    size of the column-blocked layout, and flat (instead of buffer-descriptor)
+    loads for it.  0 / False = library default."""
     sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4}[unroll]
     vsel = {0: 0, 1: 1, 2: 2, 4: 3}[vpt]
     bsel = {0: 0, 256: 1, 512: 2, 1024: 3}[bs]
     return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
-            | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0))
+            | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0)
+            | (_native.FEDAGG_FLAT if flat else 0))
 
 
 # Tuned defaults for the column-blocked reduce (profiles/r01_sweep*/: K=1000 at
@@ -318,6 +321,40 @@ def feddyn_sgd(avg: torch.Tensor, cloud: torch.Tensor, h: torch.Tensor, ratio: f
         _ptr(grad_out), cloud.numel(), _stream_ptr(cloud.device),
     )
     check(rc, "fedagg_feddyn_sgd_f32")
+    return cloud
+
+
+ALGO = {"fedavg": _native.FEDAGG_ALGO_FEDAVG, "adabest": _native.FEDAGG_ALGO_ADABEST,
+        "feddyn": _native.FEDAGG_ALGO_FEDDYN}
+
+
+def server_step(algo: str, avg: torch.Tensor, cloud: torch.Tensor, *, lr: float,
+                momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                nesterov: bool = False, maximize: bool = False, coef: float = 0.0,
+                aux: Optional[torch.Tensor] = None, avg_prev: Optional[torch.Tensor] = None,
+                momentum_buf: Optional[torch.Tensor] = None, momentum_init: bool = False,
+                grad_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused server step (include/fedagg.h fedagg_server_step_f32): the
+    algorithm's pseudo-gradient + the full torch.optim.SGD update, in place on
+    ``cloud`` (and ``aux`` / ``momentum_buf`` / ``avg_prev``).  Python scalars
+    are rounded to fp32 exactly as ATen rounds them (fl32(-lr), fl32(1-damp))."""
+    P = cloud.numel()
+    for t, n in ((avg, "avg"), (cloud, "cloud"), (aux, "aux"), (avg_prev, "avg_prev"),
+                 (momentum_buf, "momentum_buf"), (grad_out, "grad_out")):
+        if t is not None:
+            _require_hip_f32(t, n)
+            if t.numel() != P or not t.is_contiguous():
+                raise ValueError(f"{n} must be contiguous with {P} elements")
+    if algo not in ALGO:
+        raise ValueError(f"unknown algo {algo!r}")
+    sgd = _native.SgdParams(fl32(-lr), fl32(momentum), fl32(1 - dampening), fl32(weight_decay),
+                            int(bool(nesterov)), int(bool(maximize)))
+    rc = _native.load().fedagg_server_step_f32(
+        ALGO[algo], avg.data_ptr(), fl32(coef), cloud.data_ptr(), _ptr(aux), _ptr(avg_prev),
+        _ptr(momentum_buf), int(bool(momentum_init)), _ptr(grad_out), ctypes.byref(sgd), P,
+        _stream_ptr(cloud.device),
+    )
+    check(rc, "fedagg_server_step_f32")
     return cloud
 
 

@@ -70,6 +70,10 @@ extern "C" {
  * 2 = 512, 3 = 1024 lanes (float4 slots per lane = C / (4 * lanes)) */
 #define FEDAGG_BS_SHIFT 14
 #define FEDAGG_BS_MASK  0xC000
+/* blocked layout: use flat global loads instead of buffer-descriptor loads
+ * (A/B measurement switch; also taken automatically when a column block's
+ * region is >= 4 GiB) */
+#define FEDAGG_FLAT     0x10000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */

@@ -43,8 +43,10 @@ def lib():
         L.ref_fedavg_sgd_f32.argtypes = [vp, f32, vp, vp, i64]
         L.ref_adabest_sgd_f32.argtypes = [vp, f32, f32, vp, vp, vp, i64]
         L.ref_feddyn_sgd_f32.argtypes = [vp, f32, f32, vp, vp, vp, vp, i64]
+        L.ref_server_step_f32.argtypes = [ci, vp, f32, vp, vp, vp, vp, ci, vp, f32, f32, f32,
+                                          f32, ci, ci, i64]
         for fn in ("ref_reduce_f32", "ref_finalize_f32", "ref_fedavg_sgd_f32",
-                   "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32"):
+                   "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32", "ref_server_step_f32"):
             getattr(L, fn).restype = None
         _lib = L
     return _lib
@@ -122,6 +124,40 @@ def feddyn_sgd(avg: np.ndarray, cloud: np.ndarray, h: np.ndarray, weight, num_cl
     lib().ref_feddyn_sgd_f32(_p(a), float(fl32(weight / num_clients)), float(fl32(lr)), _p(c),
                              _p(hh), _p(ap), None, c.size)
     return c, hh, ap
+
+
+class ServerState(object):
+    """Oracle-side server state across rounds: cloud, the SGD momentum buffer
+    and the algorithm's auxiliary vector (AdaBest avg_params / FedDyn h)."""
+
+    ALGO = {"fedavg": 0, "adabest": 1, "feddyn": 2}
+
+    def __init__(self, algo, cloud, opt, aux=None, coef=0.0):
+        self.algo = algo
+        self.cloud = np.array(cloud, dtype=np.float32, copy=True)
+        self.opt = dict(opt)
+        self.aux = None if aux is None else np.array(aux, dtype=np.float32, copy=True)
+        self.coef = coef
+        self.buf = None
+        self.grad = None
+        self.avg_prev = None
+
+    def step(self, avg):
+        o = self.opt
+        P = self.cloud.size
+        mom = o.get("momentum", 0.0)
+        init = self.buf is None
+        if mom and init:
+            self.buf = np.empty(P, dtype=np.float32)
+        self.grad = np.empty(P, dtype=np.float32)
+        self.avg_prev = np.empty(P, dtype=np.float32) if self.algo == "feddyn" else None
+        a = np.ascontiguousarray(avg, dtype=np.float32)
+        lib().ref_server_step_f32(
+            self.ALGO[self.algo], _p(a), float(fl32(self.coef)), _p(self.cloud), _p(self.aux),
+            _p(self.avg_prev), _p(self.buf), int(init), _p(self.grad),
+            float(fl32(-o["lr"])), float(fl32(mom)), float(fl32(1 - o.get("dampening", 0.0))),
+            float(fl32(o.get("weight_decay", 0.0))), int(o.get("nesterov", False)),
+            int(o.get("maximize", False)), P)
 
 
 # ---- numpy twin (independent restatement of the reduce / divide) ----------

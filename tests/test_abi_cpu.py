@@ -43,7 +43,7 @@ def test_header_declares_the_abi():
         "fedagg_abi_version", "fedagg_strerror", "fedagg_reduce_f32", "fedagg_reduce_rows_f32",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
-        "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32",
+        "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
     ])
 
 
@@ -84,7 +84,7 @@ def test_argument_validation_without_device(lib):
     assert lib.fedagg_reduce_f32(null, 4, 16, 1, 4, null, 16, 1.0, 1, null) == E
     assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 0, null) == E  # no INIT, no acc
     assert lib.fedagg_reduce_f32(16, 2, 16, 1, 4, null, 16, 1.0, 1, null) == E  # ldx < P
-    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 1 | 0x10000, null) == E
+    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 1 | 0x100000, null) == E
     assert lib.fedagg_reduce_f32(16, 1 << 31, 16, 1, (1 << 30) + 1, null, 16, 1.0, 1, null) == E
     assert lib.fedagg_reduce_rows_f32(null, 16, 1, 4, null, 16, 1.0, 1, null) == E
     assert lib.fedagg_finalize_f32(null, 1.0, 4, 16, null) == E

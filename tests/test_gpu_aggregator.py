@@ -13,7 +13,8 @@ from oracle import vectors as V
 pytestmark = pytest.mark.gpu
 
 CASES = golden_cases()
-PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"]]
+PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"] and "opts" not in c]
+OPT_CASES = [c for c in CASES if "opts" in c]
 FLOW_CASES = [c for c in PARAM_CASES if c["P"] <= 1_100_000]
 
 
@@ -95,6 +96,56 @@ def test_algorithm_round_bitwise(case, where, dev, golden):
         assert reports.keys() == case["reports"].keys()
         for k, v in case["reports"].items():
             assert float(reports[k]) == v, k
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("case", OPT_CASES, ids=[c["id"] for c in OPT_CASES])
+def test_general_sgd_two_rounds_bitwise(case, where, dev, golden):
+    """<Algo>.optimize with torch.optim.SGD(momentum / nesterov / dampening /
+    weight_decay / maximize) for two rounds through the fused server step:
+    cloud per round, momentum buffer in optimizer.state, grad, aux — bitwise
+    equal to the reference's own optimize."""
+    from fedsim_amd.distributed.centralized import training
+    from fedsim_amd.utils import SerialAggregator, Storage
+
+    _, arrays = golden
+    algo = case["algo"]
+    cls = {"fedavg": training.FedAvg, "adabest": training.AdaBest,
+           "feddyn": training.FedDyn}[algo]
+    K, P = case["K"], case["P"]
+    X1 = V.client_rows(case["dist"], K, P, case["seed"])
+    X2 = V.client_rows(case["dist"], K, P, case["seed"] + 50)
+    weights = case["weights"]
+    cdev = dev if where == "device" else torch.device("cpu")
+    for i, opt in enumerate(case["opts"]):
+        st = Storage()
+        cloud = torch.from_numpy(V.cloud_vector(P, case["seed"] + 1)).to(cdev).requires_grad_(True)
+        optimizer = torch.optim.SGD(params=[cloud], **opt)
+        st.write("cloud_params", cloud)
+        st.write("optimizer", optimizer)
+        st.write("lr_scheduler", None)
+        if algo == "adabest":
+            st.write("avg_params", torch.from_numpy(V.cloud_vector(P, case["seed"] + 2)).to(cdev))
+            st.write("beta", case["beta"])
+        if algo == "feddyn":
+            st.write("h", torch.from_numpy(V.cloud_vector(P, case["seed"] + 3)).to(cdev))
+            st.write("num_clients", case["num_clients"])
+        for r, X in ((1, X1), (2, X2)):
+            agg = SerialAggregator()
+            msgs = V.client_messages(X, weights, device=dev if where == "device" else None)
+            _receive_all(cls, case, agg, msgs, st)
+            cls.optimize(st, agg, None)
+            _expect(case, arrays, f"cloud_o{i}_r{r}", cloud.detach().cpu().numpy())
+        if opt.get("momentum", 0):
+            buf = optimizer.state[cloud]["momentum_buffer"]
+            assert buf.device == cdev
+            _expect(case, arrays, f"mbuf_o{i}", buf.cpu().numpy())
+        if algo in ("adabest", "feddyn"):
+            _expect(case, arrays, f"avg_params_o{i}", st.read("avg_params").cpu().numpy())
+        if algo == "feddyn":
+            _expect(case, arrays, f"h_o{i}", st.read("h").cpu().numpy())
+        assert cloud.grad.device == cdev
+        _expect(case, arrays, f"grad_o{i}", cloud.grad.cpu().numpy())
 
 
 def test_zero_weight_and_diverged_rounds(dev, golden):

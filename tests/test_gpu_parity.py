@@ -11,7 +11,7 @@ from oracle import vectors as V
 pytestmark = pytest.mark.gpu
 
 CASES = golden_cases()
-PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"]]
+PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"] and "opts" not in c]
 VARIANTS = {
     "default": dict(),
     "u4v2nt": dict(unroll=4, vpt=2, nt=True),

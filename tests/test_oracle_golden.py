@@ -9,7 +9,8 @@ from oracle import ref
 from oracle import vectors as V
 
 CASES = golden_cases()
-PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"]]
+PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"] and "opts" not in c]
+OPT_CASES = [c for c in CASES if "opts" in c]
 
 
 def _inputs(case):
@@ -60,6 +61,45 @@ def test_oracle_optimize_matches_reference(case, golden):
         else:
             c = ref.fedavg_sgd(avg, cloud0, lr)
         _check(case, arrays, f"cloud_lr{lr}", c)
+
+
+def opt_case_inputs(case):
+    """Round inputs of an optimizer case (tools/gen_golden.py run_opt_case)."""
+    X1 = V.client_rows(case["dist"], case["K"], case["P"], case["seed"])
+    assert V.sha256(X1) == case["input_sha256"]
+    X2 = V.client_rows(case["dist"], case["K"], case["P"], case["seed"] + 50)
+    w = list(case["weights"])
+    if case["algo"] in ("adabest", "feddyn"):
+        w = [1] * case["K"]
+    aux, coef = None, 0.0
+    if case["algo"] == "adabest":
+        aux, coef = V.cloud_vector(case["P"], case["seed"] + 2), case["beta"]
+    elif case["algo"] == "feddyn":
+        aux, coef = V.cloud_vector(case["P"], case["seed"] + 3), sum(w) / case["num_clients"]
+    return X1, X2, w, aux, coef
+
+
+@pytest.mark.parametrize("case", OPT_CASES, ids=[c["id"] for c in OPT_CASES])
+def test_oracle_general_sgd_matches_reference(case, golden):
+    """Two rounds with momentum / nesterov / dampening / weight decay /
+    maximize server SGD: cloud per round, momentum buffer, grad, aux."""
+    _, arrays = golden
+    X1, X2, w, aux, coef = opt_case_inputs(case)
+    W = sum(w)
+    for i, opt in enumerate(case["opts"]):
+        st = ref.ServerState(case["algo"], V.cloud_vector(case["P"], case["seed"] + 1), opt,
+                             aux=aux, coef=coef)
+        for r, X in ((1, X1), (2, X2)):
+            st.step(ref.reduce(X, w, W=W))
+            _check(case, arrays, f"cloud_o{i}_r{r}", st.cloud)
+        if opt.get("momentum", 0):
+            _check(case, arrays, f"mbuf_o{i}", st.buf)
+        if case["algo"] in ("adabest",):
+            _check(case, arrays, f"avg_params_o{i}", st.aux)
+        if case["algo"] == "feddyn":
+            _check(case, arrays, f"h_o{i}", st.aux)
+            _check(case, arrays, f"avg_params_o{i}", st.avg_prev)
+        _check(case, arrays, f"grad_o{i}", st.grad)
 
 
 def test_oracle_edge_cases():

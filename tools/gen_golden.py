@@ -143,6 +143,55 @@ def run_case(R, case):
     return X, weights, out
 
 
+def run_opt_case(R, case):
+    """Two consecutive rounds of <Algo>.optimize with a general
+    torch.optim.SGD (momentum / nesterov / dampening / weight decay / maximize)
+    as the server optimizer, so the momentum buffer and AdaBest's avg_params /
+    FedDyn's h carry from round 1 into round 2."""
+    K, P, algo = case["K"], case["P"], case["algo"]
+    X1 = V.client_rows(case["dist"], K, P, case["seed"])
+    X2 = V.client_rows(case["dist"], K, P, case["seed"] + 50)
+    weights = V.client_weights(case["wkind"], K, case["seed"])
+    out = dict(ok=[True] * K, arrays={}, scalars={}, has_params=True, reports=None)
+    cls = {"fedavg": R["FedAvg"], "adabest": R["AdaBest"], "feddyn": R["FedDyn"]}[algo]
+    for i, opt in enumerate(case["opts"]):
+        st = R["Storage"]()
+        cloud = torch.from_numpy(V.cloud_vector(P, case["seed"] + 1)).requires_grad_(True)
+        optimizer = torch.optim.SGD(params=[cloud], **opt)
+        st.write("cloud_params", cloud)
+        st.write("optimizer", optimizer)
+        st.write("lr_scheduler", None)
+        if algo == "adabest":
+            st.write("avg_params", torch.from_numpy(V.cloud_vector(P, case["seed"] + 2)))
+            st.write("beta", case["beta"])
+        if algo == "feddyn":
+            st.write("h", torch.from_numpy(V.cloud_vector(P, case["seed"] + 3)))
+            st.write("num_clients", case["num_clients"])
+        for r, X in ((1, X1), (2, X2)):
+            agg = R["SerialAggregator"]()
+            for k, msg in enumerate(V.client_messages(X, weights)):
+                w = 1 if algo in ("adabest", "feddyn") else None
+                R["serial_aggregation"](st, k, msg, "train", agg, train_weight=w)
+            cls.optimize(st, agg, R["AppendixAggregator"]())
+            out["arrays"][f"cloud_o{i}_r{r}"] = cloud.detach().numpy().copy()
+        if opt.get("momentum", 0):
+            out["arrays"][f"mbuf_o{i}"] = optimizer.state[cloud]["momentum_buffer"].numpy().copy()
+        if algo in ("adabest", "feddyn"):
+            out["arrays"][f"avg_params_o{i}"] = st.read("avg_params").numpy().copy()
+        if algo == "feddyn":
+            out["arrays"][f"h_o{i}"] = st.read("h").numpy().copy()
+        out["arrays"][f"grad_o{i}"] = cloud.grad.numpy().copy()
+    return X1, weights, out
+
+
+SGD_OPTS = [
+    dict(lr=0.7, momentum=0.9),
+    dict(lr=0.5, momentum=0.9, nesterov=True),
+    dict(lr=1.0, momentum=0.5, dampening=0.1, weight_decay=1e-3),
+    dict(lr=0.3, weight_decay=0.01, maximize=True),
+]
+
+
 def build_cases():
     cases = []
     cid = 0
@@ -179,6 +228,13 @@ def build_cases():
     add(K=10, P=1_085_668, dist="realistic", wkind="adabest", algo="adabest", beta=0.6, lrs=[1.0])
     add(K=10, P=1_085_668, dist="realistic", wkind="adabest", algo="feddyn", num_clients=1000,
         lrs=[1.0])
+    # general server optimizer (momentum SGD etc.), two rounds each
+    for K, P in ((7, 1023), (64, 4099)):
+        add(K=K, P=P, dist="realistic", wkind="fedavg", algo="fedavg", opts=SGD_OPTS)
+        add(K=K, P=P, dist="realistic", wkind="adabest", algo="adabest", beta=0.6,
+            opts=SGD_OPTS)
+        add(K=K, P=P, dist="realistic", wkind="adabest", algo="feddyn", num_clients=37,
+            opts=SGD_OPTS)
     return cases
 
 
@@ -200,7 +256,7 @@ def main():
     )
     arrays = {}
     for case in build_cases():
-        X, weights, out = run_case(R, case)
+        X, weights, out = (run_opt_case if "opts" in case else run_case)(R, case)
         entry = dict(case)
         entry["weights"] = weights
         entry["input_sha256"] = V.sha256(X)

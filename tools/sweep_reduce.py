@@ -50,8 +50,8 @@ def main():
         C = a.blocked
         Xb = ops.to_blocked(Xv, C)
         bss = {1024: (256,), 2048: (256, 512), 4096: (256, 512, 1024)}[C]
-        variants = [dict(unroll=u, bs=b, nt=bool(n), table=False, blocked=C)
-                    for u, n, b in itertools.product((2, 4, 8), (0, 1), bss)]
+        variants = [dict(unroll=u, bs=b, nt=True, table=False, blocked=C, flat=f)
+                    for u, b, f in itertools.product((2, 4, 8), bss, (False, True))]
         del X, Xv, rows, table
         torch.cuda.empty_cache()
     alg = 4.0 * K * P + 4.0 * P
@@ -59,7 +59,7 @@ def main():
     for r in range(a.rounds):
         for i, var in enumerate(variants):
             fl = ops.tuning_flags(unroll=var["unroll"], vpt=var.get("vpt", 0), nt=var["nt"],
-                                  bs=var.get("bs", 0))
+                                  bs=var.get("bs", 0), flat=var.get("flat", False))
 
             def run():
                 if var.get("blocked"):
