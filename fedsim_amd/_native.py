@@ -32,6 +32,7 @@ FEDAGG_UNROLL_SHIFT = 8
 FEDAGG_VPT_SHIFT = 12
 FEDAGG_BS_SHIFT = 14
 FEDAGG_FLAT = 0x10000
+FEDAGG_LDSW = 0x20000
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0

@@ -23,8 +23,13 @@
 //     broadcast a uniform value, cheaper than an LDS round trip.
 //   * k is unrolled U-deep: U*VPT independent 16-byte loads are issued before
 //     the in-order adds consume them, so each wave keeps U*VPT KiB in flight.
-//   * The row base is uniform (SGPR pair) and the per-lane offset is 32-bit,
-//     which lets the compiler use global_load_dwordx4 v, v_off, s[base:base+1].
+//   * HBM layout: the aggregator packs client rows into a COLUMN-BLOCKED slab
+//     (one workgroup's column span holds all K rows contiguously), so each
+//     workgroup streams one contiguous region.  Those loads go through one
+//     buffer descriptor per workgroup with the row in an SGPR soffset:
+//     buffer_load_dwordx4 v, v_off, s[rsrc], s_row offen nt.
+//   * Layout / unroll / lanes-per-slot / nt were chosen by measurement
+//     (tools/sweep_reduce.py, profiles/r01_sweep*/).
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
 // (see __graft_entry__.build()).
@@ -45,6 +50,7 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 constexpr int kDefaultUnroll = 4;
 constexpr int kDefaultVptSel = 2;  // 2 float4 slots per lane
 constexpr int kDefaultBsSel = 1;   // blocked layout: 256-lane workgroups
+constexpr int kWeightTile = 2048;  // FEDAGG_LDSW ablation: weights per LDS tile
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).
@@ -181,7 +187,45 @@ __device__ __forceinline__ f32x4 div4(f32x4 a, float d) {
 //   [b*BS*VPT, (b+1)*BS*VPT); lane t of the block owns s = base + j*BS + t
 //   for j < VPT, so every wave-instruction touches 64 consecutive slots (1 KiB).
 // ---------------------------------------------------------------------------
-template <int BS, int U, int VPT, bool NT, bool GUARD, class Rows>
+// Per-client weight sources: wave-uniform scalar loads (default) or an LDS
+// tile (ablation).
+struct WeightsScalar {
+  const float* __restrict__ w;
+  __device__ __forceinline__ float operator()(int64_t k) const { return w[k]; }
+};
+struct WeightsLds {
+  const float* wsh;
+  int64_t k0;
+  __device__ __forceinline__ float operator()(int64_t k) const { return wsh[k - k0]; }
+};
+
+// Rows kb..ke-1 in order, U rows of loads in flight before the in-order adds.
+template <int U, int VPT, bool NT, class Rows, class Wf>
+__device__ __forceinline__ void accumulate_rows(const Rows& rows, const Wf& wf, int64_t kb,
+                                                int64_t ke, const uint32_t* off, f32x4* a) {
+  int64_t k = kb;
+  for (; k + U <= ke; k += U) {
+    f32x4 v[U][VPT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) v[u][j] = rows.template load4<NT>(k + u, off[j]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wk = wf(k + u);
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], v[u][j], wk);
+    }
+  }
+  for (; k < ke; ++k) {
+    const float wk = wf(k);
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], rows.template load4<NT>(k, off[j]), wk);
+  }
+}
+
+template <int BS, int U, int VPT, bool NT, bool GUARD, bool LDSW, class Rows>
 __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
                                                 const float* __restrict__ w,
                                                 int64_t B, int64_t nvec,
@@ -208,25 +252,19 @@ __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
       a[j] = ld4<false>(reinterpret_cast<const char*>(acc_in), off[j]);
   }
 
-  int64_t k = 0;
-  for (; k + U <= B; k += U) {
-    f32x4 v[U][VPT];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int j = 0; j < VPT; ++j) v[u][j] = rows.template load4<NT>(k + u, off[j]);
+  if constexpr (LDSW) {
+    // Ablation (FEDAGG_LDSW): weights staged through LDS in tiles and read
+    // back as a same-address (broadcast) ds_read, instead of s_load.
+    __shared__ float wsh[kWeightTile];
+    for (int64_t k0 = 0; k0 < B; k0 += kWeightTile) {
+      const int64_t n = (B - k0) < kWeightTile ? (B - k0) : kWeightTile;
+      __syncthreads();
+      for (int64_t i = threadIdx.x; i < n; i += BS) wsh[i] = w[k0 + i];
+      __syncthreads();
+      accumulate_rows<U, VPT, NT>(rows, WeightsLds{wsh, k0}, k0, k0 + n, off, a);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float wk = w[k + u];
-#pragma unroll
-      for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], v[u][j], wk);
-    }
-  }
-  for (; k < B; ++k) {
-    const float wk = w[k];
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) a[j] = axpy_rn4(a[j], rows.template load4<NT>(k, off[j]), wk);
+  } else {
+    accumulate_rows<U, VPT, NT>(rows, WeightsScalar{w}, 0, B, off, a);
   }
 
   if (flags & FEDAGG_FINALIZE) {
@@ -253,7 +291,7 @@ __device__ __forceinline__ void reduce_scalar_cols(const Rows& rows,
   out[col] = a;
 }
 
-template <int BS, int U, int VPT, bool NT, class Rows>
+template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false>
 __global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
                                                        const float* __restrict__ w,
                                                        int64_t B, int64_t nvec,
@@ -263,9 +301,9 @@ __global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
   const int64_t block_start = static_cast<int64_t>(blockIdx.x) * (BS * VPT);
   const int64_t block_end = block_start + BS * VPT;
   if (block_end <= nvec) {
-    reduce_vec_body<BS, U, VPT, NT, false>(rows, w, B, nvec, acc_in, out, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, false, LDSW>(rows, w, B, nvec, acc_in, out, W32, flags);
   } else if (block_start < nvec) {
-    reduce_vec_body<BS, U, VPT, NT, true>(rows, w, B, nvec, acc_in, out, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, true, LDSW>(rows, w, B, nvec, acc_in, out, W32, flags);
   }
   // The last block also owns the (P % 4) scalar tail columns.
   if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
@@ -474,7 +512,7 @@ inline int elementwise_grid(int64_t n) {
   return static_cast<int>(g);
 }
 
-template <int BS, int U, int VPT, bool NT, class Rows>
+template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false>
 hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
                       const float* acc_in, float* out, float W32, int flags,
                       hipStream_t s) {
@@ -484,7 +522,7 @@ hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
   // workgroup whose column span contains it (matters for RowsBlocked)
   int64_t grid = (nvec + (tail > 0 ? 1 : 0) + BS * VPT - 1) / (BS * VPT);
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows, LDSW>), dim3(static_cast<unsigned>(grid)),
                      dim3(BS), 0, s, rows, w, B, nvec, tail, acc_in, out, W32, flags);
   return hipGetLastError();
 }
@@ -559,7 +597,7 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (B > 0 && !w) return FEDAGG_EINVAL;
   if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
-                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT))
+                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW))
     return FEDAGG_EINVAL;
   return 0;
 }
@@ -622,7 +660,12 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   hipError_t e;
   // buffer-descriptor path unless asked for flat loads or a block region is
   // too large for a 32-bit descriptor range
-  if ((flags & FEDAGG_FLAT) || Kcap * C * 4 >= (int64_t(1) << 32)) {
+  if (flags & FEDAGG_LDSW) {
+    // ablation: only the default configuration (C=4096, 256 lanes, U=4, nt)
+    if (C != 4096 || Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
+    e = launch_vec<256, 4, 4, true, RowsBlockedBuf, true>(RowsBlockedBuf{Xb, Kcap, C}, w, B, P,
+                                                          acc_in, out, W32, flags, s);
+  } else if ((flags & FEDAGG_FLAT) || Kcap * C * 4 >= (int64_t(1) << 32)) {
     e = dispatch_blocked(RowsBlocked{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags, s);
   } else {
     e = dispatch_blocked(RowsBlockedBuf{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags,

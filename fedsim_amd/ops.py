@@ -40,7 +40,7 @@ def fl32(x) -> float:
 
 
 def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
-                 flat: bool = False) -> int:
+                 flat: bool = False, ldsw: bool = False) -> int:
     """Kernel tuning bits (include/fedagg.h): k-unroll, float4 slots per lane
     (row-major / pointer-table layouts), non-temporal loads, the workgroup
     size of the column-blocked layout, and flat (instead of buffer-descriptor)
@@ -50,7 +50,7 @@ def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
     bsel = {0: 0, 256: 1, 512: 2, 1024: 3}[bs]
     return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
             | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0)
-            | (_native.FEDAGG_FLAT if flat else 0))
+            | (_native.FEDAGG_FLAT if flat else 0) | (_native.FEDAGG_LDSW if ldsw else 0))
 
 
 # Tuned defaults for the column-blocked reduce (profiles/r01_sweep*/: K=1000 at
@@ -194,16 +194,18 @@ def blocked_shape(K: int, P: int, C: int = 2048):
     return ((P + C - 1) // C, K, C)
 
 
-def to_blocked(X: torch.Tensor, C: int = 2048) -> torch.Tensor:
-    """Repack a [K, P] tensor into the column-blocked layout (copy)."""
+def to_blocked(X: torch.Tensor, C: int = 2048, kcap: Optional[int] = None) -> torch.Tensor:
+    """Repack a [K, P] tensor into the column-blocked layout (copy), with
+    ``kcap`` >= K rows of capacity per column block (rows K.. are zero)."""
     K, P = X.shape
+    kcap = K if kcap is None else kcap
     nb, _, _ = blocked_shape(K, P, C)
-    Xb = torch.zeros((nb, K, C), dtype=X.dtype, device=X.device)
+    Xb = torch.zeros((nb, kcap, C), dtype=X.dtype, device=X.device)
     full = P // C
     if full:
-        Xb[:full].copy_(X[:, : full * C].reshape(K, full, C).transpose(0, 1))
+        Xb[:full, :K].copy_(X[:, : full * C].reshape(K, full, C).transpose(0, 1))
     if P % C:
-        Xb[full, :, : P % C].copy_(X[:, full * C:])
+        Xb[full, :K, : P % C].copy_(X[:, full * C:])
     return Xb
 
 

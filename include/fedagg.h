@@ -74,6 +74,9 @@ extern "C" {
  * (A/B measurement switch; also taken automatically when a column block's
  * region is >= 4 GiB) */
 #define FEDAGG_FLAT     0x10000
+/* ablation: stage the per-client weights through LDS tiles instead of reading
+ * them with wave-uniform scalar loads (same results; A/B measurement switch) */
+#define FEDAGG_LDSW     0x20000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */

@@ -23,6 +23,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--table", action="store_true", help="also time the row-table kernel")
+    ap.add_argument("--only-default", action="store_true")
+    ap.add_argument("--kcap-pad", type=int, default=0,
+                    help="extra (unused) rows per column block of the blocked slab")
+    ap.add_argument("--pad-pair", type=int, default=None,
+                    help="also time a copy of the slab with this many extra rows, interleaved")
     ap.add_argument("--blocked", type=int, default=0,
                     help="time only the column-blocked layout with this C (1024/2048/4096)")
     a = ap.parse_args()
@@ -48,22 +53,37 @@ def main():
     Xb = None
     if a.blocked:
         C = a.blocked
-        Xb = ops.to_blocked(Xv, C)
+        Xb = ops.to_blocked(Xv, C, kcap=K + a.kcap_pad)
         bss = {1024: (256,), 2048: (256, 512), 4096: (256, 512, 1024)}[C]
         variants = [dict(unroll=u, bs=b, nt=True, table=False, blocked=C, flat=f)
                     for u, b, f in itertools.product((2, 4, 8), bss, (False, True))]
+        if C == 4096:  # ablation: weights staged in LDS instead of scalar loads
+            variants.append(dict(unroll=4, bs=256, nt=True, table=False, blocked=C, flat=False,
+                                 ldsw=True))
+        if a.only_default:
+            variants = [dict(unroll=4, bs=256, nt=True, table=False, blocked=C, flat=False)]
         del X, Xv, rows, table
         torch.cuda.empty_cache()
+        slabs = {a.kcap_pad: Xb}
+        if a.pad_pair is not None:
+            # same data in a second slab with a different row capacity,
+            # timed interleaved with the first (one process, rule 24)
+            Xb2 = torch.zeros((Xb.shape[0], K + a.pad_pair, C), device=dev)
+            Xb2[:, :K].copy_(Xb[:, :K])
+            slabs[a.pad_pair] = Xb2
+            variants = [dict(v, kcap_pad=p) for p in slabs for v in variants]
     alg = 4.0 * K * P + 4.0 * P
     times = {i: [] for i in range(len(variants))}
     for r in range(a.rounds):
         for i, var in enumerate(variants):
             fl = ops.tuning_flags(unroll=var["unroll"], vpt=var.get("vpt", 0), nt=var["nt"],
-                                  bs=var.get("bs", 0), flat=var.get("flat", False))
+                                  bs=var.get("bs", 0), flat=var.get("flat", False),
+                                  ldsw=var.get("ldsw", False))
 
             def run():
                 if var.get("blocked"):
-                    ops.reduce_blocked(Xb, w32, out, W=1.0, flags=fl)
+                    ops.reduce_blocked(slabs[var.get("kcap_pad", a.kcap_pad)], w32, out, B=K,
+                                       W=1.0, flags=fl)
                 elif var["table"]:
                     ops.reduce_rows(rows, w32, out, W=1.0, flags=fl, table=table)
                 else:
