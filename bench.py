@@ -1,11 +1,14 @@
 """Benchmark: client-update bytes/s reduced (device-resident), K clients x P params.
 
-One step = one FedAvg server round on the MI355X, device-resident:
-  weighted exact-mode reduction of K client rows (+ the pop divide, fused in
-  the same pass) -> avg, then the fused FedAvg SGD epilogue on cloud_params.
-This is SerialAggregator.add x K + pop + FedAvg.optimize of the reference
-(fedsim/utils/aggregators.py:23-122, fedsim/distributed/centralized/training/fedavg.py:193-208)
-with the client vectors already packed in HBM.
+One step = one FedAvg server round on the MI355X, device-resident: the
+weighted exact-mode reduction of K client rows, the pop divide and the FedAvg
+server SGD step (pseudo-gradient stored as cloud.grad) in ONE pass over the
+slab (fedagg_reduce_step_blocked_f32) -- what SerialAggregator.add x K +
+FedAvg.optimize does in this package.  Reference: SerialAggregator.add / pop
+(fedsim/utils/aggregators.py:23-122) + FedAvg.optimize
+(fedsim/distributed/centralized/training/fedavg.py:193-208), with the client
+vectors already packed in HBM.  --step split times the two-launch variant
+(reduce + divide, then the epilogue kernel).
 
 Multi-GPU (launched by torch.distributed.run): parameter-sharded weak scaling,
 SURVEY §8e — rank g owns a contiguous P-column shard of an N*P-parameter model
@@ -50,6 +53,9 @@ def parse():
     ap.add_argument("--vpt", type=int, default=2, choices=[0, 1, 2, 4],
                     help="float4 slots per lane (strided layout only)")
     ap.add_argument("--nt", type=int, default=1)
+    ap.add_argument("--step", default="fused", choices=["fused", "split"],
+                    help="fused: server step inside the reduce pass (the product path); "
+                         "split: reduce + divide, then a separate epilogue launch")
     ap.add_argument("--no-epilogue", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -63,7 +69,10 @@ def dist_setup():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     pg = None
-    if world > 1:
+    # any torch.distributed.run launch (even --nproc-per-node 1) takes the
+    # process-group path, so the N=1 rehearsal exercises the same barrier /
+    # max-over-ranks code the N>1 runs use
+    if world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ):
         import torch.distributed as dist
 
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
@@ -106,14 +115,14 @@ def make_inputs(K, P, rank, dev, layout, C):
     return X, weights
 
 
-def load_pmc(path, K, P, flags, layout):
+def load_pmc(path, K, P, flags, layout, step):
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
     if d.get("K") == K and d.get("P") == P and d.get("flags") == flags and \
-            d.get("layout", "strided") == layout:
+            d.get("layout", "strided") == layout and d.get("step", "split") == step:
         return d.get("hbm_bytes_per_launch")
     return None
 
@@ -164,15 +173,23 @@ def main():
     K, P = a.K, a.P
     flags = ops.tuning_flags(unroll=a.unroll, vpt=a.vpt if a.layout == "strided" else 0,
                              nt=bool(a.nt))
+    fused = a.step == "fused" and a.layout == "blocked" and not a.no_epilogue
+    step_mode = "fused" if fused else "split"
     X, weights = make_inputs(K, P, rank, dev, a.layout, a.C)
     W = sum(weights)
     w32 = torch.tensor([ops.fl32(v) for v in weights], dtype=torch.float32, device=dev)
     avg = torch.empty(P, dtype=torch.float32, device=dev)
     cloud = torch.zeros(P, dtype=torch.float32, device=dev)
+    grad = torch.empty(P, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # FedAvg.optimize's server step (default SGD lr 1.0, fed_learn.py:129),
+    # cloud.grad = pseudo-gradient as torch leaves it
+    sstep = ops.ServerStep("fedavg", cloud, lr=1.0, grad_out=grad)
 
     def reduce():
-        if a.layout == "strided":
+        if fused:
+            ops.reduce_blocked_step(X, w32, sstep, W=W)
+        elif a.layout == "strided":
             ops.reduce_slab(X[:, :P], w32, avg, W=W, P=P, flags=flags)
         else:
             ops.reduce_blocked(X, w32, avg, W=W, flags=flags)
@@ -183,8 +200,8 @@ def main():
         reduce()
         if ev is not None:
             ev[1].record(stream)
-        if not a.no_epilogue:
-            ops.fedavg_sgd(avg, cloud, 1.0)
+        if not a.no_epilogue and not fused:
+            ops.fedavg_sgd(avg, cloud, 1.0, grad_out=grad)
 
     for _ in range(a.warmup):
         step()
@@ -209,10 +226,12 @@ def main():
 
     total_bytes = 4.0 * K * P * world
     value = total_bytes * a.steps / elapsed / 1e9
-    alg_bytes_launch = 4.0 * K * P + 4.0 * P + 4.0 * K
+    # client rows + weights, plus per column: fused = cloud read + cloud write +
+    # grad write; split (reduce kernel alone) = the average's write
+    alg_bytes_launch = 4.0 * K * P + 4.0 * K + (12.0 * P if fused else 4.0 * P)
     achieved = alg_bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = load_pmc(a.pmc_json, K, P, flags,
-                       a.layout if a.layout == "strided" else f"blocked{a.C}")
+                       a.layout if a.layout == "strided" else f"blocked{a.C}", step_mode)
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -227,8 +246,11 @@ def main():
         "dtype": "f32",
         "data": "synthetic (x_k = base + eps_k on device, FedAvg int weights U{50..600})",
         "config": {
-            "workload": "FedAvg server round, device-resident: exact weighted reduce + divide "
-                        "(fused) + fused SGD step",
+            "workload": ("FedAvg server round, device-resident: exact weighted reduce + divide "
+                         "+ SGD server step in one pass" if fused else
+                         "FedAvg server round, device-resident: exact weighted reduce + divide, "
+                         "then the SGD epilogue kernel"),
+            "step": step_mode,
             "clients_K": K,
             "params_per_gpu_P": P,
             "params_total": P * world,
@@ -240,6 +262,7 @@ def main():
         "roofline": {
             "bound": "hbm",
             "kernel": "k_reduce_vec (%s)" % (
+                "fedagg_reduce_step_blocked_f32, EpiStep<FEDAVG>" if fused else
                 "fedagg_reduce_blocked_f32" if a.layout == "blocked" else "fedagg_reduce_f32"),
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBPS,

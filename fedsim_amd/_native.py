@@ -53,6 +53,23 @@ class SgdParams(ctypes.Structure):
     ]
 
 
+class StepArgs(ctypes.Structure):
+    """struct fedagg_step_args (include/fedagg.h)."""
+
+    _fields_ = [
+        ("algo", ctypes.c_int),
+        ("coef", ctypes.c_float),
+        ("cloud", ctypes.c_void_p),
+        ("aux", ctypes.c_void_p),
+        ("avg_prev", ctypes.c_void_p),
+        ("momentum_buf", ctypes.c_void_p),
+        ("momentum_init", ctypes.c_int),
+        ("grad_out", ctypes.c_void_p),
+        ("avg_out", ctypes.c_void_p),
+        ("sgd", SgdParams),
+    ]
+
+
 # (name, restype, argtypes) for every symbol include/fedagg.h declares.
 SIGNATURES = {
     "fedagg_abi_version": (ctypes.c_int, []),
@@ -100,6 +117,12 @@ SIGNATURES = {
         [ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
          ctypes.POINTER(SgdParams), ctypes.c_int64, ctypes.c_void_p],
+    ),
+    "fedagg_reduce_step_blocked_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
+         ctypes.POINTER(StepArgs), ctypes.c_void_p],
     ),
     "fedagg_feddyn_sgd_f32": (
         ctypes.c_int,

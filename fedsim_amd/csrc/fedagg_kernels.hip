@@ -182,6 +182,129 @@ __device__ __forceinline__ f32x4 div4(f32x4 a, float d) {
 }
 
 // ---------------------------------------------------------------------------
+// Server step: the algorithm's pseudo-gradient followed by the full
+// torch.optim.SGD single-tensor update (torch/optim/sgd.py _single_tensor_sgd,
+// the path torch takes for CPU params), with every ATen op's rounding:
+//   d = maximize ? -g : g
+//   d = fma(param, wd, d)                         grad.add(param, alpha=wd)
+//   buf = first ? d : fma(d, 1-damp, fl(buf*m))   buf.mul_(m).add_(d, alpha=1-damp)
+//   d = nesterov ? fma(buf, m, d) : buf           grad.add(buf, alpha=m)
+//   param = fma(d, -lr, param)                    param.add_(d, alpha=-lr)
+// ---------------------------------------------------------------------------
+struct SgdArgs {
+  float neg_lr, momentum, one_minus_damp, wd;
+  int nesterov, maximize, first;
+};
+
+struct StepOut {
+  float cloud, g, aux, buf;
+};
+
+// One column: a = average, c = cloud, x = aux (AdaBest avg_params / FedDyn h),
+// b = momentum buffer.
+template <int ALGO, bool MOM>
+__device__ __forceinline__ StepOut step_math(float a, float c, float x, float b, float coef,
+                                             const SgdArgs& sa) {
+  StepOut o;
+  float g;
+  if constexpr (ALGO == FEDAGG_ALGO_FEDAVG) {
+    g = c - a;  // fedavg.py:199
+    o.aux = x;
+  } else if constexpr (ALGO == FEDAGG_ALGO_ADABEST) {
+    const float h = coef * (x - a);  // adabest.py:178-180
+    const float nw = a - h;
+    g = c - nw;
+    o.aux = a;  // avg_params <- avg (adabest.py:188)
+  } else {
+    const float g1 = c - a;  // feddyn.py:176-184
+    const float hn = x + coef * g1;
+    const float nw = a - hn;
+    g = c - nw;
+    o.aux = hn;
+  }
+  o.g = g;
+  float d = sa.maximize ? -g : g;
+  if (sa.wd != 0.f) d = __builtin_fmaf(c, sa.wd, d);
+  o.buf = b;
+  if constexpr (MOM) {
+    const float nb = sa.first ? d : __builtin_fmaf(d, sa.one_minus_damp, b * sa.momentum);
+    o.buf = nb;
+    d = sa.nesterov ? __builtin_fmaf(nb, sa.momentum, d) : nb;
+  }
+  o.cloud = __builtin_fmaf(d, sa.neg_lr, c);
+  return o;
+}
+
+// ---------------------------------------------------------------------------
+// Epilogues: what a kernel does with a finished column value (the average, or
+// the raw sum).  `off` is the column's byte offset in a [P] vector.
+// ---------------------------------------------------------------------------
+struct EpiStore {  // plain reduce: store it
+  float* out;
+  __device__ __forceinline__ void vec(int64_t off, f32x4 a) const {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(out) + off) = a;
+  }
+  __device__ __forceinline__ void one(int64_t col, float a) const { out[col] = a; }
+};
+
+struct StepPtrs {
+  float* cloud;
+  float* aux;
+  float* avg_prev;
+  float* buf;
+  float* grad;
+  float* avg_out;
+  float coef;
+  SgdArgs sa;
+};
+
+template <int ALGO, bool MOM>
+struct EpiStep {  // server step on the average, in registers
+  static constexpr int kAlgo = ALGO;
+  static constexpr bool kMom = MOM;
+  StepPtrs p;
+  __device__ __forceinline__ void one(int64_t i, float a) const {
+    const float x = (ALGO != FEDAGG_ALGO_FEDAVG) ? p.aux[i] : 0.f;
+    const float b = MOM ? p.buf[i] : 0.f;
+    const StepOut o = step_math<ALGO, MOM>(a, p.cloud[i], x, b, p.coef, p.sa);
+    if (p.avg_out) p.avg_out[i] = a;
+    if (p.grad) p.grad[i] = o.g;
+    if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) p.aux[i] = o.aux;
+    if constexpr (ALGO == FEDAGG_ALGO_FEDDYN) {
+      if (p.avg_prev) p.avg_prev[i] = a;
+    }
+    if constexpr (MOM) p.buf[i] = o.buf;
+    p.cloud[i] = o.cloud;
+  }
+  __device__ __forceinline__ void vec(int64_t off, f32x4 a) const {
+    auto at = [off](float* q) {
+      return reinterpret_cast<f32x4*>(reinterpret_cast<char*>(q) + off);
+    };
+    const f32x4 c = *at(p.cloud);
+    f32x4 x = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) x = *at(p.aux);
+    if constexpr (MOM) b = *at(p.buf);
+    f32x4 nc, g, nx, nb;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const StepOut o = step_math<ALGO, MOM>(a[e], c[e], x[e], b[e], p.coef, p.sa);
+      nc[e] = o.cloud;
+      g[e] = o.g;
+      nx[e] = o.aux;
+      nb[e] = o.buf;
+    }
+    if (p.avg_out) *at(p.avg_out) = a;
+    if (p.grad) *at(p.grad) = g;
+    if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) *at(p.aux) = nx;
+    if constexpr (ALGO == FEDAGG_ALGO_FEDDYN) {
+      if (p.avg_prev) *at(p.avg_prev) = a;
+    }
+    if constexpr (MOM) *at(p.buf) = nb;
+    *at(p.cloud) = nc;
+  }
+};
+
+// ---------------------------------------------------------------------------
 // Exact-mode reduction, f32x4 slots.
 //   slot s covers columns [4s, 4s+4).  Block b (BS lanes) owns slots
 //   [b*BS*VPT, (b+1)*BS*VPT); lane t of the block owns s = base + j*BS + t
@@ -225,11 +348,11 @@ __device__ __forceinline__ void accumulate_rows(const Rows& rows, const Wf& wf, 
   }
 }
 
-template <int BS, int U, int VPT, bool NT, bool GUARD, bool LDSW, class Rows>
+template <int BS, int U, int VPT, bool NT, bool GUARD, bool LDSW, class Rows, class Epi>
 __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
                                                 const float* __restrict__ w,
                                                 int64_t B, int64_t nvec,
-                                                const float* acc_in, float* out,
+                                                const float* acc_in, const Epi& epi,
                                                 float W32, int flags) {
   const int64_t base = static_cast<int64_t>(blockIdx.x) * (BS * VPT) + threadIdx.x;
   uint32_t off[VPT];
@@ -273,41 +396,41 @@ __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
   }
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
-    if (ok[j]) *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(out) + off[j]) = a[j];
+    if (ok[j]) epi.vec(off[j], a[j]);
   }
 }
 
 // Scalar columns [col0, col0 + ncols): the P % 4 tail of the f32x4 path.
-template <bool NT, class Rows>
+template <bool NT, class Rows, class Epi>
 __device__ __forceinline__ void reduce_scalar_cols(const Rows& rows,
                                                    const float* __restrict__ w,
                                                    int64_t B, int64_t col,
-                                                   const float* acc_in, float* out,
+                                                   const float* acc_in, const Epi& epi,
                                                    float W32, int flags) {
   const uint32_t off = static_cast<uint32_t>(col) * 4u;
   float a = (flags & FEDAGG_INIT) ? 0.f : acc_in[col];
   for (int64_t k = 0; k < B; ++k) a = axpy_rn(a, ld1<NT>(rows.row(k), off), w[k]);
   if (flags & FEDAGG_FINALIZE) a = a / W32;
-  out[col] = a;
+  epi.one(col, a);
 }
 
-template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false>
+template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false, class Epi = EpiStore>
 __global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
                                                        const float* __restrict__ w,
                                                        int64_t B, int64_t nvec,
                                                        int tail, const float* acc_in,
-                                                       float* out, float W32,
+                                                       Epi epi, float W32,
                                                        int flags) {
   const int64_t block_start = static_cast<int64_t>(blockIdx.x) * (BS * VPT);
   const int64_t block_end = block_start + BS * VPT;
   if (block_end <= nvec) {
-    reduce_vec_body<BS, U, VPT, NT, false, LDSW>(rows, w, B, nvec, acc_in, out, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, false, LDSW>(rows, w, B, nvec, acc_in, epi, W32, flags);
   } else if (block_start < nvec) {
-    reduce_vec_body<BS, U, VPT, NT, true, LDSW>(rows, w, B, nvec, acc_in, out, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, true, LDSW>(rows, w, B, nvec, acc_in, epi, W32, flags);
   }
   // The last block also owns the (P % 4) scalar tail columns.
   if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
-    reduce_scalar_cols<NT>(rows, w, B, nvec * 4 + threadIdx.x, acc_in, out, W32, flags);
+    reduce_scalar_cols<NT>(rows, w, B, nvec * 4 + threadIdx.x, acc_in, epi, W32, flags);
 }
 
 // Generic path for rows that are not 16-byte aligned: one column per lane,
@@ -321,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(Rows rows,
                                                           int flags) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (c >= P) return;
-  reduce_scalar_cols<false>(rows, w, B, c, acc_in, out, W32, flags);
+  reduce_scalar_cols<false>(rows, w, B, c, acc_in, EpiStore{out}, W32, flags);
 }
 
 // ---------------------------------------------------------------------------
@@ -446,57 +569,24 @@ __global__ __launch_bounds__(kBlock) void k_feddyn_sgd(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// General fused server step: algorithm pseudo-gradient + the full
-// torch.optim.SGD single-tensor update (torch/optim/sgd.py _single_tensor_sgd,
-// the path torch takes for CPU params), with every ATen op's rounding:
-//   d = maximize ? -g : g
-//   d = fma(param, wd, d)                         grad.add(param, alpha=wd)
-//   buf = first ? d : fma(d, 1-damp, fl(buf*m))   buf.mul_(m).add_(d, alpha=1-damp)
-//   d = nesterov ? fma(buf, m, d) : buf           grad.add(buf, alpha=m)
-//   param = fma(d, -lr, param)                    param.add_(d, alpha=-lr)
+// General server step over a stored average (fedagg_server_step_f32): the
+// EpiStep epilogue applied to avg[], f32x4 when every operand is 16-B aligned.
 // ---------------------------------------------------------------------------
-struct SgdArgs {
-  float neg_lr, momentum, one_minus_damp, wd;
-  int nesterov, maximize, first;
-};
-
-template <int ALGO, bool MOM>
+template <int ALGO, bool MOM, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_server_step(const float* __restrict__ avg,
-                                                        float coef, float* __restrict__ cloud,
-                                                        float* __restrict__ aux,
-                                                        float* __restrict__ avg_prev,
-                                                        float* __restrict__ buf,
-                                                        float* __restrict__ grad_out,
-                                                        SgdArgs sa, int64_t P) {
+                                                        EpiStep<ALGO, MOM> epi, int64_t P) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < P; i += stride) {
-    const float a = avg[i];
-    const float c = cloud[i];
-    float g;
-    if constexpr (ALGO == FEDAGG_ALGO_FEDAVG) {
-      g = c - a;  // fedavg.py:199
-    } else if constexpr (ALGO == FEDAGG_ALGO_ADABEST) {
-      const float h = coef * (aux[i] - a);  // adabest.py:178-180
-      const float nw = a - h;
-      g = c - nw;
-      aux[i] = a;  // avg_params <- avg (adabest.py:188)
-    } else {
-      const float g1 = c - a;  // feddyn.py:176-184
-      const float hn = aux[i] + coef * g1;
-      const float nw = a - hn;
-      g = c - nw;
-      aux[i] = hn;
-      if (avg_prev) avg_prev[i] = a;
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if constexpr (VEC) {
+    const int64_t nvec = P / 4;
+    for (int64_t i = t0; i < nvec; i += stride)
+      epi.vec(i * 16, reinterpret_cast<const f32x4*>(avg)[i]);
+    if (blockIdx.x == 0 && static_cast<int64_t>(threadIdx.x) < P - nvec * 4) {
+      const int64_t c = nvec * 4 + threadIdx.x;
+      epi.one(c, avg[c]);
     }
-    if (grad_out) grad_out[i] = g;
-    float d = sa.maximize ? -g : g;
-    if (sa.wd != 0.f) d = __builtin_fmaf(c, sa.wd, d);
-    if constexpr (MOM) {
-      const float b = sa.first ? d : __builtin_fmaf(d, sa.one_minus_damp, buf[i] * sa.momentum);
-      buf[i] = b;
-      d = sa.nesterov ? __builtin_fmaf(b, sa.momentum, d) : b;
-    }
-    cloud[i] = __builtin_fmaf(d, sa.neg_lr, c);
+  } else {
+    for (int64_t i = t0; i < P; i += stride) epi.one(i, avg[i]);
   }
 }
 
@@ -512,9 +602,9 @@ inline int elementwise_grid(int64_t n) {
   return static_cast<int>(g);
 }
 
-template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false>
+template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false, class Epi = EpiStore>
 hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
-                      const float* acc_in, float* out, float W32, int flags,
+                      const float* acc_in, const Epi& epi, float W32, int flags,
                       hipStream_t s) {
   const int64_t nvec = P / 4;
   const int tail = static_cast<int>(P - nvec * 4);
@@ -522,8 +612,9 @@ hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
   // workgroup whose column span contains it (matters for RowsBlocked)
   int64_t grid = (nvec + (tail > 0 ? 1 : 0) + BS * VPT - 1) / (BS * VPT);
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows, LDSW>), dim3(static_cast<unsigned>(grid)),
-                     dim3(BS), 0, s, rows, w, B, nvec, tail, acc_in, out, W32, flags);
+  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows, LDSW, Epi>),
+                     dim3(static_cast<unsigned>(grid)), dim3(BS), 0, s, rows, w, B, nvec, tail,
+                     acc_in, epi, W32, flags);
   return hipGetLastError();
 }
 
@@ -531,14 +622,15 @@ template <int BS, int VPT, bool NT, class Rows>
 hipError_t dispatch_unroll(int unroll_sel, const Rows& rows, const float* w, int64_t B,
                            int64_t P, const float* acc_in, float* out, float W32,
                            int flags, hipStream_t s) {
+  const EpiStore st{out};
   switch (unroll_sel) {
-    case 1: return launch_vec<BS, 4, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
-    case 2: return launch_vec<BS, 8, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
-    case 3: return launch_vec<BS, 16, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
-    case 4: return launch_vec<BS, 2, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+    case 1: return launch_vec<BS, 4, VPT, NT>(rows, w, B, P, acc_in, st, W32, flags, s);
+    case 2: return launch_vec<BS, 8, VPT, NT>(rows, w, B, P, acc_in, st, W32, flags, s);
+    case 3: return launch_vec<BS, 16, VPT, NT>(rows, w, B, P, acc_in, st, W32, flags, s);
+    case 4: return launch_vec<BS, 2, VPT, NT>(rows, w, B, P, acc_in, st, W32, flags, s);
     case 0:
     default:
-      return launch_vec<BS, kDefaultUnroll, VPT, NT>(rows, w, B, P, acc_in, out, W32, flags, s);
+      return launch_vec<BS, kDefaultUnroll, VPT, NT>(rows, w, B, P, acc_in, st, W32, flags, s);
   }
 }
 
@@ -600,6 +692,47 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
                 FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW))
     return FEDAGG_EINVAL;
   return 0;
+}
+
+// Validate a server step's operands and pack them for EpiStep.
+int make_step(int algo, float coef, float* cloud, float* aux, float* avg_prev, float* buf,
+              int momentum_init, float* grad, float* avg_out, const fedagg_sgd_params* sgd,
+              StepPtrs* sp, bool* mom) {
+  if (!sgd || !cloud) return FEDAGG_EINVAL;
+  if (algo != FEDAGG_ALGO_FEDAVG && algo != FEDAGG_ALGO_ADABEST && algo != FEDAGG_ALGO_FEDDYN)
+    return FEDAGG_EINVAL;
+  if (algo != FEDAGG_ALGO_FEDAVG && !aux) return FEDAGG_EINVAL;
+  *mom = sgd->momentum != 0.f;
+  if (*mom && !buf) return FEDAGG_EINVAL;
+  if (sgd->nesterov && (!*mom || sgd->one_minus_dampening != 1.f)) return FEDAGG_EINVAL;
+  *sp = StepPtrs{cloud, aux, avg_prev, buf, grad, avg_out, coef,
+                 SgdArgs{sgd->neg_lr, sgd->momentum, sgd->one_minus_dampening, sgd->weight_decay,
+                         sgd->nesterov, sgd->maximize, momentum_init}};
+  return 0;
+}
+
+bool step_aligned(const StepPtrs& p) {
+  for (const float* q : {p.cloud, p.aux, p.avg_prev, p.buf, p.grad, p.avg_out})
+    if (q && !aligned16(q)) return false;
+  return true;
+}
+
+// f(EpiStep<ALGO, MOM>{sp}) for the runtime (algo, mom).
+template <class F>
+hipError_t with_step(int algo, bool mom, const StepPtrs& sp, F&& f) {
+  switch (algo) {
+    case FEDAGG_ALGO_FEDAVG:
+      return mom ? f(EpiStep<FEDAGG_ALGO_FEDAVG, true>{sp})
+                 : f(EpiStep<FEDAGG_ALGO_FEDAVG, false>{sp});
+    case FEDAGG_ALGO_ADABEST:
+      return mom ? f(EpiStep<FEDAGG_ALGO_ADABEST, true>{sp})
+                 : f(EpiStep<FEDAGG_ALGO_ADABEST, false>{sp});
+    case FEDAGG_ALGO_FEDDYN:
+      return mom ? f(EpiStep<FEDAGG_ALGO_FEDDYN, true>{sp})
+                 : f(EpiStep<FEDAGG_ALGO_FEDDYN, false>{sp});
+    default:
+      return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace
@@ -664,7 +797,7 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
     // ablation: only the default configuration (C=4096, 256 lanes, U=4, nt)
     if (C != 4096 || Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
     e = launch_vec<256, 4, 4, true, RowsBlockedBuf, true>(RowsBlockedBuf{Xb, Kcap, C}, w, B, P,
-                                                          acc_in, out, W32, flags, s);
+                                                          acc_in, EpiStore{out}, W32, flags, s);
   } else if ((flags & FEDAGG_FLAT) || Kcap * C * 4 >= (int64_t(1) << 32)) {
     e = dispatch_blocked(RowsBlocked{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags, s);
   } else {
@@ -745,32 +878,64 @@ int fedagg_server_step_f32(int algo, const float* avg, float coef, float* cloud,
                            float* avg_prev, float* momentum_buf, int momentum_init,
                            float* grad_out, const fedagg_sgd_params* sgd, int64_t P,
                            void* stream) {
-  if (P < 0 || !sgd) return FEDAGG_EINVAL;
+  if (P < 0) return FEDAGG_EINVAL;
+  StepPtrs sp;
+  bool mom;
+  int rc = make_step(algo, coef, cloud, aux, avg_prev, momentum_buf, momentum_init, grad_out,
+                     nullptr, sgd, &sp, &mom);
+  if (rc != 0) return rc;
   if (P == 0) return 0;
-  if (!avg || !cloud) return FEDAGG_EINVAL;
-  if (algo != FEDAGG_ALGO_FEDAVG && !aux) return FEDAGG_EINVAL;
-  const bool mom = sgd->momentum != 0.f;
-  if (mom && !momentum_buf) return FEDAGG_EINVAL;
-  if (sgd->nesterov && (!mom || sgd->one_minus_dampening != 1.f)) return FEDAGG_EINVAL;
-  SgdArgs sa{sgd->neg_lr, sgd->momentum, sgd->one_minus_dampening, sgd->weight_decay,
-             sgd->nesterov, sgd->maximize, momentum_init};
+  if (!avg) return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 g(elementwise_grid(P)), b(kBlock);
-#define FEDAGG_STEP(A)                                                                    \
-  if (mom)                                                                                \
-    hipLaunchKernelGGL((k_server_step<A, true>), g, b, 0, s, avg, coef, cloud, aux,      \
-                       avg_prev, momentum_buf, grad_out, sa, P);                          \
-  else                                                                                    \
-    hipLaunchKernelGGL((k_server_step<A, false>), g, b, 0, s, avg, coef, cloud, aux,     \
-                       avg_prev, momentum_buf, grad_out, sa, P);
-  switch (algo) {
-    case FEDAGG_ALGO_FEDAVG: FEDAGG_STEP(FEDAGG_ALGO_FEDAVG) break;
-    case FEDAGG_ALGO_ADABEST: FEDAGG_STEP(FEDAGG_ALGO_ADABEST) break;
-    case FEDAGG_ALGO_FEDDYN: FEDAGG_STEP(FEDAGG_ALGO_FEDDYN) break;
-    default: return FEDAGG_EINVAL;
-  }
-#undef FEDAGG_STEP
-  return static_cast<int>(hipGetLastError());
+  const bool vec = aligned16(avg) && step_aligned(sp);
+  const dim3 g(elementwise_grid(vec ? P / 4 + 1 : P)), b(kBlock);
+  hipError_t e = with_step(algo, mom, sp, [&](auto epi) {
+    constexpr int A = decltype(epi)::kAlgo;
+    constexpr bool M = decltype(epi)::kMom;
+    if (vec)
+      hipLaunchKernelGGL((k_server_step<A, M, true>), g, b, 0, s, avg, epi, P);
+    else
+      hipLaunchKernelGGL((k_server_step<A, M, false>), g, b, 0, s, avg, epi, P);
+    return hipGetLastError();
+  });
+  if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
+  return static_cast<int>(e);
+}
+
+int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
+                                   int64_t B, int64_t P, const float* acc_in, float W32,
+                                   int flags, const fedagg_step_args* step, void* stream) {
+  if (!step) return FEDAGG_EINVAL;
+  StepPtrs sp;
+  bool mom;
+  int rc = make_step(step->algo, step->coef, step->cloud, step->aux, step->avg_prev,
+                     step->momentum_buf, step->momentum_init, step->grad_out, step->avg_out,
+                     &step->sgd, &sp, &mom);
+  if (rc != 0) return rc;
+  rc = check_reduce_args(w, B, P, acc_in, step->cloud, flags);
+  if (rc != 0 || P == 0) return rc;
+  if (flags & (FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
+  if (B > Kcap || (B > 0 && !Xb)) return FEDAGG_EINVAL;
+  if (Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
+  if (!aligned16(Xb) || !step_aligned(sp) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in)))
+    return FEDAGG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const RowsBlockedBuf rows{Xb, Kcap, C};
+  // the per-C default configuration of fedagg_reduce_blocked_f32 (256 lanes,
+  // VPT = C/1024, U = 4 at C=4096 else 2, non-temporal loads)
+  hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+    switch (C) {
+      case 4096: return launch_vec<256, 4, 4, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
+                                                                          epi, W32, flags, s);
+      case 2048: return launch_vec<256, 2, 2, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
+                                                                          epi, W32, flags, s);
+      case 1024: return launch_vec<256, 2, 1, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
+                                                                          epi, W32, flags, s);
+      default: return hipErrorInvalidValue;
+    }
+  });
+  if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
+  return static_cast<int>(e);
 }
 
 int fedagg_feddyn_sgd_f32(const float* avg, float ratio, float lr, float* cloud, float* h,

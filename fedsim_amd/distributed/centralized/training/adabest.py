@@ -86,17 +86,17 @@ class AdaBest(FedAvg):
     def optimize(server_storage, serial_aggregator, appendix_aggregator):
         if "local_params" in serial_aggregator:
             beta = server_storage.read("beta")
-            param_avg = pop_average(serial_aggregator)
             optimizer = server_storage.read("optimizer")
             lr_scheduler = server_storage.read("lr_scheduler")
             cloud_params = server_storage.read("cloud_params")
             avg_params = server_storage.read("avg_params")
             cfg = sgd_config(optimizer, cloud_params)
             if cfg is not None:
-                new_avg, _ = fused_server_step("adabest", cloud_params, param_avg, optimizer,
+                new_avg, _ = fused_server_step("adabest", cloud_params,
+                                               (serial_aggregator, "local_params"), optimizer,
                                                cfg, coef=beta, aux=avg_params)
             else:
-                param_avg = param_avg.to(cloud_params.device)
+                param_avg = pop_average(serial_aggregator).to(cloud_params.device)
                 h = beta * (avg_params - param_avg)
                 new_params = param_avg - h
                 optimizer.zero_grad()

@@ -84,21 +84,23 @@ class FedAvg(CentralFLAlgorithm):
 
     def optimize(server_storage, serial_aggregator, appendix_aggregator):
         if "local_params" in serial_aggregator:
-            param_avg = pop_average(serial_aggregator)
             optimizer = server_storage.read("optimizer")
             lr_scheduler = server_storage.read("lr_scheduler")
             cloud_params = server_storage.read("cloud_params")
             cfg = sgd_config(optimizer, cloud_params)
             if cfg is not None:
-                fused_server_step("fedavg", cloud_params, param_avg, optimizer, cfg)
+                # pop + pseudo-gradient + SGD step in the round's last reduce pass
+                fused_server_step("fedavg", cloud_params, (serial_aggregator, "local_params"),
+                                  optimizer, cfg)
             else:
+                param_avg = pop_average(serial_aggregator)
                 pseudo_grads = cloud_params.data - param_avg.to(cloud_params.device)
                 optimizer.zero_grad()
                 cloud_params.grad = pseudo_grads
                 optimizer.step()
+                del param_avg
             if lr_scheduler is not None:
                 lr_scheduler.step()
-            del param_avg
         return serial_aggregator.pop_all()
 
     def deploy(server_storage):

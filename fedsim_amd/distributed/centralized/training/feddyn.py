@@ -76,7 +76,6 @@ class FedDyn(FedAvg):
     def optimize(server_storage, serial_aggregator, appendix_aggregator):
         if "local_params" in serial_aggregator:
             weight = serial_aggregator.get_weight("local_params")
-            param_avg = pop_average(serial_aggregator)
             optimizer = server_storage.read("optimizer")
             lr_scheduler = server_storage.read("lr_scheduler")
             cloud_params = server_storage.read("cloud_params")
@@ -85,11 +84,12 @@ class FedDyn(FedAvg):
             server_storage.change_protection("num_clients", False, False)
             cfg = sgd_config(optimizer, cloud_params)
             if cfg is not None:
-                h, new_avg = fused_server_step("feddyn", cloud_params, param_avg, optimizer,
+                h, new_avg = fused_server_step("feddyn", cloud_params,
+                                               (serial_aggregator, "local_params"), optimizer,
                                                cfg, coef=weight / num_clients, aux=h,
                                                want_avg_prev=True)
             else:
-                param_avg = param_avg.to(cloud_params.device)
+                param_avg = pop_average(serial_aggregator).to(cloud_params.device)
                 pseudo_grads = cloud_params.data - param_avg
                 h = h + weight / num_clients * pseudo_grads
                 new_params = param_avg - h
@@ -101,7 +101,6 @@ class FedDyn(FedAvg):
                 lr_scheduler.step()
             server_storage.write("avg_params", new_avg)
             server_storage.write("h", h.data)
-            del param_avg
         return serial_aggregator.pop_all()
 
     def deploy(server_storage):

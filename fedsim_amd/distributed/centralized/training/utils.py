@@ -113,18 +113,29 @@ def _work_copy(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
     return t.detach().reshape(-1).to(dev, copy=True).contiguous()
 
 
-def fused_server_step(algo: str, cloud: torch.Tensor, avg: torch.Tensor, optimizer,
+def fused_server_step(algo: str, cloud: torch.Tensor, avg, optimizer,
                       cfg: dict, coef: float = 0.0, aux: Optional[torch.Tensor] = None,
                       want_avg_prev: bool = False):
     """One kernel: algorithm pseudo-gradient + SGD update of ``cloud``.
+
+    ``avg`` is the averaged tensor, or ``(aggregator, key)``: then the key is
+    popped and, when the aggregator is ours, the step runs fused into the
+    round's last reduction pass (the average is never stored).
 
     Leaves ``cloud.grad`` = pseudo-gradient and the momentum buffer in
     ``optimizer.state[cloud]`` exactly as ``optimizer.step()`` would, and marks
     the optimizer as stepped for LR schedulers.  Returns ``(aux', avg_prev')``
     on the devices of ``aux`` / ``cloud`` (None where not requested)."""
-    dev = _hip_device_for(avg, cloud)
+    source = None
+    if isinstance(avg, tuple):
+        source, avg = avg, None
+        agg, key = source
+        dev = agg.device_of(key) if isinstance(agg, _DeviceSerialAggregator) else None
+        if dev is None:
+            avg, source = agg.pop(key), None
+    if source is None:
+        dev = _hip_device_for(avg, cloud)
     c = cloud.data if cloud.device == dev else cloud.data.to(dev)
-    a = (avg if avg.device == dev else avg.to(dev)).reshape(-1).contiguous()
     x = _work_copy(aux, dev) if aux is not None else None
     ap = torch.empty_like(c) if want_avg_prev else None
     g = torch.empty_like(c)
@@ -134,10 +145,14 @@ def fused_server_step(algo: str, cloud: torch.Tensor, avg: torch.Tensor, optimiz
         prev = state.get("momentum_buffer")
         init = prev is None
         buf = torch.empty_like(c) if init else _work_copy(prev, dev)
-    ops.server_step(algo, a, c, lr=cfg["lr"], momentum=cfg["momentum"],
-                    dampening=cfg["dampening"], weight_decay=cfg["weight_decay"],
-                    nesterov=cfg["nesterov"], maximize=cfg["maximize"], coef=coef, aux=x,
-                    avg_prev=ap, momentum_buf=buf, momentum_init=init, grad_out=g)
+    step = ops.ServerStep(algo, c.view(-1), lr=cfg["lr"], momentum=cfg["momentum"],
+                          dampening=cfg["dampening"], weight_decay=cfg["weight_decay"],
+                          nesterov=cfg["nesterov"], maximize=cfg["maximize"], coef=coef,
+                          aux=x, avg_prev=ap, momentum_buf=buf, momentum_init=init, grad_out=g)
+    if source is not None:
+        agg.pop_step(key, step)
+    else:
+        step.apply((avg if avg.device == dev else avg.to(dev)).reshape(-1).contiguous())
     if c is not cloud.data:
         cloud.data.copy_(c)
     optimizer.zero_grad()

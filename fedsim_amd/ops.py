@@ -330,34 +330,117 @@ ALGO = {"fedavg": _native.FEDAGG_ALGO_FEDAVG, "adabest": _native.FEDAGG_ALGO_ADA
         "feddyn": _native.FEDAGG_ALGO_FEDDYN}
 
 
-def server_step(algo: str, avg: torch.Tensor, cloud: torch.Tensor, *, lr: float,
-                momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-                nesterov: bool = False, maximize: bool = False, coef: float = 0.0,
-                aux: Optional[torch.Tensor] = None, avg_prev: Optional[torch.Tensor] = None,
-                momentum_buf: Optional[torch.Tensor] = None, momentum_init: bool = False,
-                grad_out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Fused server step (include/fedagg.h fedagg_server_step_f32): the
-    algorithm's pseudo-gradient + the full torch.optim.SGD update, in place on
-    ``cloud`` (and ``aux`` / ``momentum_buf`` / ``avg_prev``).  Python scalars
-    are rounded to fp32 exactly as ATen rounds them (fl32(-lr), fl32(1-damp))."""
-    P = cloud.numel()
-    for t, n in ((avg, "avg"), (cloud, "cloud"), (aux, "aux"), (avg_prev, "avg_prev"),
-                 (momentum_buf, "momentum_buf"), (grad_out, "grad_out")):
-        if t is not None:
-            _require_hip_f32(t, n)
-            if t.numel() != P or not t.is_contiguous():
-                raise ValueError(f"{n} must be contiguous with {P} elements")
-    if algo not in ALGO:
-        raise ValueError(f"unknown algo {algo!r}")
-    sgd = _native.SgdParams(fl32(-lr), fl32(momentum), fl32(1 - dampening), fl32(weight_decay),
-                            int(bool(nesterov)), int(bool(maximize)))
-    rc = _native.load().fedagg_server_step_f32(
-        ALGO[algo], avg.data_ptr(), fl32(coef), cloud.data_ptr(), _ptr(aux), _ptr(avg_prev),
-        _ptr(momentum_buf), int(bool(momentum_init)), _ptr(grad_out), ctypes.byref(sgd), P,
-        _stream_ptr(cloud.device),
+class ServerStep(object):
+    """The operands of one server step (include/fedagg.h fedagg_step_args):
+    the algorithm's pseudo-gradient + the full torch.optim.SGD update, in place
+    on ``cloud`` (and ``aux`` / ``momentum_buf`` / ``avg_prev``).  Python
+    scalars are rounded to fp32 exactly as ATen rounds them (fl32(-lr),
+    fl32(1-damp)).
+
+    ``apply(avg)`` runs it on a stored average (fedagg_server_step_f32);
+    ``reduce_blocked_step(..., step)`` runs it fused into the last drain of a
+    round, so the average never round-trips through HBM."""
+
+    def __init__(self, algo: str, cloud: torch.Tensor, *, lr: float, momentum: float = 0.0,
+                 dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+                 maximize: bool = False, coef: float = 0.0,
+                 aux: Optional[torch.Tensor] = None, avg_prev: Optional[torch.Tensor] = None,
+                 momentum_buf: Optional[torch.Tensor] = None, momentum_init: bool = False,
+                 grad_out: Optional[torch.Tensor] = None,
+                 avg_out: Optional[torch.Tensor] = None) -> None:
+        if algo not in ALGO:
+            raise ValueError(f"unknown algo {algo!r}")
+        self.P = P = cloud.numel()
+        self.cloud = cloud
+        operands = ((cloud, "cloud"), (aux, "aux"), (avg_prev, "avg_prev"),
+                    (momentum_buf, "momentum_buf"), (grad_out, "grad_out"), (avg_out, "avg_out"))
+        for t, n in operands:
+            if t is not None:
+                _require_hip_f32(t, n)
+                if t.numel() != P or not t.is_contiguous():
+                    raise ValueError(f"{n} must be contiguous with {P} elements")
+                if t.device != cloud.device:
+                    raise ValueError(f"{n} is on {t.device}, cloud on {cloud.device}")
+        self._keep = [t for t, _ in operands if t is not None]  # alive until launched
+        self.sgd = _native.SgdParams(fl32(-lr), fl32(momentum), fl32(1 - dampening),
+                                     fl32(weight_decay), int(bool(nesterov)),
+                                     int(bool(maximize)))
+        self.args = _native.StepArgs(ALGO[algo], fl32(coef), cloud.data_ptr(), _ptr(aux),
+                                     _ptr(avg_prev), _ptr(momentum_buf),
+                                     int(bool(momentum_init)), _ptr(grad_out), _ptr(avg_out),
+                                     self.sgd)
+
+    def aligned(self) -> bool:
+        """Every operand 16-B aligned (required by the fused entry)."""
+        return all(t.data_ptr() % 16 == 0 for t in self._keep)
+
+    def apply(self, avg: torch.Tensor) -> torch.Tensor:
+        _require_hip_f32(avg, "avg")
+        if avg.numel() != self.P or not avg.is_contiguous():
+            raise ValueError(f"avg must be contiguous with {self.P} elements")
+        a = self.args
+        rc = _native.load().fedagg_server_step_f32(
+            a.algo, avg.data_ptr(), a.coef, a.cloud, a.aux, a.avg_prev, a.momentum_buf,
+            a.momentum_init, a.grad_out, ctypes.byref(self.sgd), self.P,
+            _stream_ptr(self.cloud.device),
+        )
+        check(rc, "fedagg_server_step_f32")
+        return self.cloud
+
+
+def server_step(algo: str, avg: torch.Tensor, cloud: torch.Tensor, **kw) -> torch.Tensor:
+    """ServerStep(algo, cloud, **kw).apply(avg)  (fedagg_server_step_f32)."""
+    return ServerStep(algo, cloud, **kw).apply(avg)
+
+
+def can_fuse_step(Xb: torch.Tensor, step: ServerStep) -> bool:
+    """Whether fedagg_reduce_step_blocked_f32 accepts this slab and step."""
+    return (Xb.dim() == 3 and Xb.shape[2] in BLOCK_COLS
+            and Xb.shape[1] * Xb.shape[2] * 4 < (1 << 32) and step.aligned()
+            and Xb.device == step.cloud.device)
+
+
+def reduce_blocked_step(
+    Xb: torch.Tensor,
+    w32: torch.Tensor,
+    step: ServerStep,
+    B: Optional[int] = None,
+    acc_in: Optional[torch.Tensor] = None,
+    W: Optional[float] = None,
+    r0: int = 0,
+) -> torch.Tensor:
+    """reduce_blocked(..., out=avg) then step.apply(avg), fused into one pass
+    (fedagg_reduce_step_blocked_f32).  Returns step.cloud."""
+    _require_hip_f32(Xb, "Xb")
+    _require_hip_f32(w32, "w32")
+    if Xb.dim() != 3 or not Xb.is_contiguous():
+        raise ValueError("Xb must be a contiguous [nblk, Kcap, C] tensor")
+    nb, Kcap, C = Xb.shape
+    P = step.P
+    if nb != (P + C - 1) // C:
+        raise ValueError("Xb block count does not match the step's length")
+    B = Kcap - r0 if B is None else B
+    if w32.numel() < B:
+        raise ValueError("w32 too short")
+    if r0 < 0 or B < 0 or r0 + B > Kcap:
+        raise ValueError("row range outside the slab")
+    f = 0
+    if acc_in is None:
+        f |= FEDAGG_INIT
+    else:
+        _require_hip_f32(acc_in, "acc_in")
+        if acc_in.numel() != P:
+            raise ValueError("acc_in size mismatch")
+    W32 = 0.0
+    if W is not None:
+        f |= FEDAGG_FINALIZE
+        W32 = fl32(W)
+    rc = _native.load().fedagg_reduce_step_blocked_f32(
+        Xb.data_ptr() + 4 * r0 * C, Kcap, C, w32.data_ptr(), B, P, _ptr(acc_in), W32, f,
+        ctypes.byref(step.args), _stream_ptr(Xb.device),
     )
-    check(rc, "fedagg_server_step_f32")
-    return cloud
+    check(rc, "fedagg_reduce_step_blocked_f32")
+    return step.cloud
 
 
 def adabest_sgd(avg: torch.Tensor, cloud: torch.Tensor, avg_prev: torch.Tensor,

@@ -204,9 +204,11 @@ class _DeviceEntry(object):
         self.pending_w.append(w32)
         self.cur_w = new_w
 
-    def _flush(self, final_W) -> None:
+    def _flush(self, final_W, step: Optional[ops.ServerStep] = None) -> None:
         """Reduce the pending rows into acc (arrival order); divide by
-        fl32(final_W) in the same pass if given."""
+        fl32(final_W) in the same pass if given.  With ``step``, the last
+        segment's pass also runs the server step on the result instead of
+        storing it (pop + optimize in one pass; needs n_pending > 0)."""
         n = self.n_pending
         cur = torch.cuda.current_stream(self.dev)
         if n == 0:
@@ -216,11 +218,7 @@ class _DeviceEntry(object):
         if self.copy_event is not None:
             cur.wait_event(self.copy_event)
             self.copy_event = None
-        if self.acc is None:
-            self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
-            acc_in = None
-        else:
-            acc_in = self.acc
+        acc_in = self.acc
         w32 = torch.tensor(self.pending_w, dtype=torch.float32).pin_memory()
         w32 = w32.to(self.dev, non_blocking=True)
         first = self.R - self.tail
@@ -228,9 +226,16 @@ class _DeviceEntry(object):
         off = 0
         for i, (r0, cnt) in enumerate(segs):
             last = i == len(segs) - 1
-            ops.reduce_blocked(self.slab, w32[off:off + cnt], self.acc, B=cnt, acc_in=acc_in,
-                               W=final_W if last else None, flags=self.flags, r0=r0)
-            acc_in = self.acc
+            if last and step is not None:
+                ops.reduce_blocked_step(self.slab, w32[off:off + cnt], step, B=cnt,
+                                        acc_in=acc_in, W=final_W, r0=r0)
+            else:
+                if self.acc is None:
+                    self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
+                ops.reduce_blocked(self.slab, w32[off:off + cnt], self.acc, B=cnt,
+                                   acc_in=acc_in, W=final_W if last else None,
+                                   flags=self.flags, r0=r0)
+                acc_in = self.acc
             off += cnt
         ev = torch.cuda.Event()
         ev.record(cur)
@@ -265,6 +270,16 @@ class _DeviceEntry(object):
         self.slab = None
         self.acc = None
         return out
+
+    def pop_step(self, step: ops.ServerStep) -> None:
+        """pop(on_device=True) followed by step.apply(avg), fused into the last
+        drain when rows are pending and the step's operands allow it."""
+        if self.n_pending == 0 or not ops.can_fuse_step(self.slab, step):
+            step.apply(self.pop(on_device=True).reshape(-1))
+            return
+        self._flush(final_W=self.cur_w if self._weighted() else None, step=step)
+        self.slab = None
+        self.acc = None
 
 
 class SerialAggregator(object):
@@ -372,6 +387,27 @@ class SerialAggregator(object):
         del self._members[key]
         return e.pop(on_device=True)
 
+    def device_of(self, key) -> Optional[torch.device]:
+        """HIP device holding a tensor key's sum (None for host keys)."""
+        e = self._entry(key)
+        return e.dev if isinstance(e, _DeviceEntry) else None
+
+    def pop_step(self, key, step: ops.ServerStep) -> None:
+        """``pop(key)`` and ``step.apply(average)`` in one pass over the
+        pending client rows (not part of the reference API): the server step
+        of FedAvg / AdaBest / FedNova / FedDyn optimize runs in the epilogue of
+        the round's last reduction, so the average is never stored."""
+        e = self._entry(key)
+        if not isinstance(e, _DeviceEntry):
+            avg = self.pop(key)
+            step.apply(avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+            return
+        del self._members[key]
+        if e.dev != step.cloud.device:
+            step.apply(e.pop(on_device=True).reshape(-1).to(step.cloud.device))
+            return
+        e.pop_step(step)
+
     def items(self):
         for key in self._members.keys():
             yield key, self.get(key)
@@ -437,6 +473,27 @@ class AppendixAggregator(object):
         self._check(key)
         list_v, list_w, _ = self._members.pop(key)
         return sum(v * w for v, w in zip(list_v, list_w)) / sum(list_w)
+
+    def device_of(self, key) -> Optional[torch.device]:
+        """HIP device holding a tensor key's sum (None for host keys)."""
+        e = self._entry(key)
+        return e.dev if isinstance(e, _DeviceEntry) else None
+
+    def pop_step(self, key, step: ops.ServerStep) -> None:
+        """``pop(key)`` and ``step.apply(average)`` in one pass over the
+        pending client rows (not part of the reference API): the server step
+        of FedAvg / AdaBest / FedNova / FedDyn optimize runs in the epilogue of
+        the round's last reduction, so the average is never stored."""
+        e = self._entry(key)
+        if not isinstance(e, _DeviceEntry):
+            avg = self.pop(key)
+            step.apply(avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+            return
+        del self._members[key]
+        if e.dev != step.cloud.device:
+            step.apply(e.pop(on_device=True).reshape(-1).to(step.cloud.device))
+            return
+        e.pop_step(step)
 
     def items(self):
         for key in self._members.keys():

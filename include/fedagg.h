@@ -28,6 +28,9 @@
  *   fedagg_server_step_f32
  *       the three optimize epilogues above with any torch.optim.SGD
  *       configuration (momentum / nesterov / weight decay / maximize)
+ *   fedagg_reduce_step_blocked_f32
+ *       SerialAggregator.pop + optimize fused: the round's last drain and the
+ *       server step in one pass              aggregators.py:104-122 + fedavg.py:193-208
  *
  * Bit-exactness contract (exact mode, the default): every output equals the
  * reference CPU aggregation bit for bit, given the same arrival order:
@@ -221,6 +224,40 @@ int fedagg_server_step_f32(int algo, const float* avg, float coef, float* cloud,
                            float* avg_prev, float* momentum_buf, int momentum_init,
                            float* grad_out, const fedagg_sgd_params* sgd, int64_t P,
                            void* stream);
+
+/*
+ * The operands of one server step, for the fused reduce + step entry below.
+ * Same meaning as the fedagg_server_step_f32 arguments; avg_out (optional)
+ * additionally receives the average itself.
+ */
+typedef struct fedagg_step_args {
+  int algo;               /* FEDAGG_ALGO_*                                     */
+  float coef;             /* AdaBest beta / FedDyn weight/num_clients          */
+  float* cloud;           /* [P] in/out, required                              */
+  float* aux;             /* [P] in/out: AdaBest avg_params / FedDyn h         */
+  float* avg_prev;        /* [P] out, FedDyn only, optional                    */
+  float* momentum_buf;    /* [P] in/out, required iff sgd.momentum != 0        */
+  int momentum_init;      /* != 0: no momentum buffer yet (buf <- d)           */
+  float* grad_out;        /* [P] out, optional: the pseudo-gradient g          */
+  float* avg_out;         /* [P] out, optional: the average                    */
+  fedagg_sgd_params sgd;
+} fedagg_step_args;
+
+/*
+ * The last drain of a round fused with the server step:
+ *     fedagg_reduce_blocked_f32(..., out = avg)  then  fedagg_server_step_f32(avg, ...)
+ * in ONE pass over the slab. The average never round-trips through HBM.
+ * It replaces SerialAggregator.pop (aggregators.py:104-122) followed by the
+ * algorithm's optimize (fedavg.py:193-208, adabest.py:172-189,
+ * feddyn.py:157-194), with bit-identical results to the two-call sequence.
+ * Flags: FEDAGG_INIT / FEDAGG_FINALIZE as for the reduce. The tuning bits are
+ * ignored (the per-C default configuration is used). FEDAGG_FLAT / FEDAGG_LDSW /
+ * FEDAGG_SCALAR are rejected. Every [P] operand must be 16-byte aligned, and a
+ * column block's region (Kcap * C * 4 bytes) must be < 4 GiB.
+ */
+int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
+                                   int64_t B, int64_t P, const float* acc_in, float W32,
+                                   int flags, const fedagg_step_args* step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -44,6 +44,7 @@ def test_header_declares_the_abi():
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
+        "fedagg_reduce_step_blocked_f32",
     ])
 
 
@@ -91,6 +92,28 @@ def test_argument_validation_without_device(lib):
     assert lib.fedagg_finalize_f32(16, 1.0, -1, 16, null) == E
     assert lib.fedagg_fedavg_sgd_f32(16, 1.0, 17, null, 4, null) == E  # misaligned
     assert lib.fedagg_adabest_sgd_f32(16, 0.6, 1.0, 16, null, null, 4, null) == E
+    # fused reduce + step: missing / malformed step operands
+    from fedsim_amd import _native
+
+    sgd = _native.SgdParams(-1.0, 0.0, 1.0, 0.0, 0, 0)
+    ok = _native.StepArgs(0, 0.0, 16, None, None, None, 0, None, None, sgd)
+    rs = lib.fedagg_reduce_step_blocked_f32
+    assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3, None, null) == E  # no step
+    no_cloud = _native.StepArgs(0, 0.0, None, None, None, None, 0, None, None, sgd)
+    assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(no_cloud), null) == E
+    ada_no_aux = _native.StepArgs(1, 0.6, 16, None, None, None, 0, None, None, sgd)
+    assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(ada_no_aux), null) == E
+    mom = _native.SgdParams(-1.0, 0.9, 1.0, 0.0, 0, 0)
+    no_buf = _native.StepArgs(0, 0.0, 16, None, None, None, 1, None, None, mom)
+    assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(no_buf), null) == E
+    assert rs(16, 4, 3000, 16, 1, 4, null, 1.0, 3, ctypes.byref(ok), null) == E  # bad C
+    assert rs(16, 4, 4096, 16, 5, 4, null, 1.0, 3, ctypes.byref(ok), null) == E  # B > Kcap
+    assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3 | 0x10000, ctypes.byref(ok), null) == E
+    assert rs(16, 1 << 18, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(ok), null) == E  # 4 GiB
+    misaligned = _native.StepArgs(0, 0.0, 20, None, None, None, 0, None, None, sgd)
+    assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(misaligned), null) == E
+    assert lib.fedagg_server_step_f32(0, 16, 0.0, 16, null, null, null, 0, null, None, 4,
+                                      null) == E  # no sgd params
     # P == 0 is a no-op success
     assert lib.fedagg_reduce_f32(null, 0, null, 0, 0, null, null, 1.0, 1, null) == 0
     assert lib.fedagg_finalize_f32(null, 1.0, 0, null, null) == 0

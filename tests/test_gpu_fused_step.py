@@ -1,0 +1,202 @@
+"""GPU parity of the fused last-drain + server step
+(fedagg_reduce_step_blocked_f32): the oracle's reduce -> divide -> server
+step sequence (oracle/fedagg_ref.c, restating aggregators.py:17-122 and
+fedavg.py / adabest.py / feddyn.py optimize with torch.optim.SGD) is
+reproduced bit for bit, for every algorithm x SGD configuration x column-block
+width, with ring segments chained through the accumulator and P % 4 tails."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits
+from oracle import ref
+from oracle import vectors as V
+
+pytestmark = pytest.mark.gpu
+
+OPTS = {
+    "plain_lr0.3": dict(lr=0.3),
+    "momentum_first": dict(lr=0.5, momentum=0.9),
+    "momentum_damp_wd": dict(lr=0.1, momentum=0.8, dampening=0.25, weight_decay=1e-3),
+    "nesterov": dict(lr=0.7, momentum=0.5, nesterov=True),
+    "maximize_wd": dict(lr=1.0, weight_decay=0.01, maximize=True),
+}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from fedsim_amd import _native
+
+    _native.load()
+    return torch.device("cuda:0")
+
+
+def _setup(algo, opt, P, seed, prebuf):
+    """Oracle state and the matching device operands."""
+    aux = V.cloud_vector(P, seed + 2) if algo != "fedavg" else None
+    coef = 0.6 if algo == "adabest" else (0.37 if algo == "feddyn" else 0.0)
+    st = ref.ServerState(algo, V.cloud_vector(P, seed + 1), opt, aux=aux, coef=coef)
+    if prebuf and opt.get("momentum"):
+        st.buf = V.cloud_vector(P, seed + 4)
+    return st, coef
+
+
+def _step_for(st, coef, algo, opt, dev, want_avg):
+    from fedsim_amd import ops
+
+    P = st.cloud.size
+    t = lambda a: torch.from_numpy(np.array(a, dtype=np.float32, copy=True)).to(dev)  # noqa: E731
+    cloud = t(st.cloud)
+    aux = t(st.aux) if st.aux is not None else None
+    mom = opt.get("momentum", 0.0)
+    buf = None
+    if mom:
+        buf = t(st.buf) if st.buf is not None else torch.empty(P, device=dev)
+    d = dict(cloud=cloud, aux=aux, buf=buf, grad=torch.empty(P, device=dev),
+             avg_prev=torch.empty(P, device=dev) if algo == "feddyn" else None,
+             avg=torch.empty(P, device=dev) if want_avg else None)
+    step = ops.ServerStep(algo, cloud, lr=opt["lr"], momentum=mom,
+                          dampening=opt.get("dampening", 0.0),
+                          weight_decay=opt.get("weight_decay", 0.0),
+                          nesterov=opt.get("nesterov", False), maximize=opt.get("maximize", False),
+                          coef=coef, aux=aux, avg_prev=d["avg_prev"], momentum_buf=buf,
+                          momentum_init=(mom != 0 and st.buf is None), grad_out=d["grad"],
+                          avg_out=d["avg"])
+    return step, d
+
+
+def _check(st, avg, d, algo, opt):
+    np.testing.assert_array_equal(bits(d["cloud"].cpu().numpy()), bits(st.cloud))
+    np.testing.assert_array_equal(bits(d["grad"].cpu().numpy()), bits(st.grad))
+    if st.aux is not None:
+        np.testing.assert_array_equal(bits(d["aux"].cpu().numpy()), bits(st.aux))
+    if opt.get("momentum"):
+        np.testing.assert_array_equal(bits(d["buf"].cpu().numpy()), bits(st.buf))
+    if algo == "feddyn":
+        np.testing.assert_array_equal(bits(d["avg_prev"].cpu().numpy()), bits(st.avg_prev))
+    if d["avg"] is not None:
+        np.testing.assert_array_equal(bits(d["avg"].cpu().numpy()), bits(avg))
+
+
+@pytest.mark.parametrize("C", [1024, 2048, 4096])
+@pytest.mark.parametrize("P", [1, 5, 4099, 70_001])
+@pytest.mark.parametrize("opt", list(OPTS))
+@pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
+def test_reduce_step_bitwise(algo, opt, P, C, dev):
+    from fedsim_amd import ops
+
+    o = OPTS[opt]
+    K = 13
+    seed = 1000 + P % 97 + C
+    X = V.client_rows("realistic", K, P, seed)
+    w = V.client_weights("fedavg", K, seed)
+    W = sum(w)
+    avg = ref.reduce(X, w, W=W)
+    st, coef = _setup(algo, o, P, seed, prebuf=(opt == "momentum_damp_wd"))
+    step, d = _step_for(st, coef, algo, o, dev, want_avg=(P != 4099))
+    st.step(avg)
+    Xb = ops.to_blocked(torch.from_numpy(X).to(dev), C, kcap=K + 2)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    # two ring segments: rows 0..h-1 into an accumulator, the rest fused
+    h = K // 3
+    acc = torch.empty(P, device=dev)
+    ops.reduce_blocked(Xb, w32[:h].contiguous(), acc, B=h)
+    ops.reduce_blocked_step(Xb, w32[h:].contiguous(), step, B=K - h, acc_in=acc, W=W, r0=h)
+    _check(st, avg, d, algo, o)
+
+
+@pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
+def test_reduce_step_single_pass_and_raw_sum(algo, dev):
+    """Whole slab in one fused pass (FEDAGG_INIT), and W=None (no divide)."""
+    from fedsim_amd import ops
+
+    K, P, C = 7, 9_999, 2048
+    X = V.client_rows("normal", K, P, 9)
+    w = V.client_weights("fedavg", K, 9)
+    Xb = ops.to_blocked(torch.from_numpy(X).to(dev), C)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    for W in (sum(w), None):
+        o = OPTS["momentum_first"]
+        avg = ref.reduce(X, w, W=W)
+        st, coef = _setup(algo, o, P, 9, prebuf=False)
+        step, d = _step_for(st, coef, algo, o, dev, want_avg=True)
+        st.step(avg)
+        ops.reduce_blocked_step(Xb, w32, step, W=W)
+        _check(st, avg, d, algo, o)
+
+
+def test_server_step_unaligned_operands(dev):
+    """fedagg_server_step_f32 on 4-byte-offset views takes the scalar kernel;
+    same bits as the oracle."""
+    from fedsim_amd import ops
+
+    P = 1031
+    o = OPTS["nesterov"]
+    st, coef = _setup("adabest", o, P, 3, prebuf=False)
+    avg = V.cloud_vector(P, 8)
+    big = torch.zeros(4, P + 1, device=dev)
+    cloud, aux, buf, avg_d = (big[i, 1:] for i in range(4))
+    cloud.copy_(torch.from_numpy(st.cloud))
+    aux.copy_(torch.from_numpy(st.aux))
+    avg_d.copy_(torch.from_numpy(avg))
+    grad = torch.empty(P, device=dev)
+    ops.server_step("adabest", avg_d, cloud, lr=o["lr"], momentum=o["momentum"], nesterov=True,
+                    coef=coef, aux=aux, momentum_buf=buf, momentum_init=True, grad_out=grad)
+    st.step(avg)
+    np.testing.assert_array_equal(bits(cloud.cpu().numpy()), bits(st.cloud))
+    np.testing.assert_array_equal(bits(aux.cpu().numpy()), bits(st.aux))
+    np.testing.assert_array_equal(bits(buf.cpu().numpy()), bits(st.buf))
+    np.testing.assert_array_equal(bits(grad.cpu().numpy()), bits(st.grad))
+
+
+@pytest.mark.parametrize("max_rows", [3, 5, 64])
+def test_aggregator_pop_step_ring(max_rows, dev):
+    """SerialAggregator.pop_step through a wrapped ring (two segments, the
+    second fused) equals pop + step in the oracle."""
+    from fedsim_amd import ops
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 11, 20_011
+    X = V.client_rows("realistic", K, P, 21)
+    w = V.client_weights("fedavg", K, 21)
+    agg = SerialAggregator(max_rows=max_rows)
+    for k in range(K):
+        agg.add("local_params", torch.from_numpy(X[k].copy()).to(dev), w[k])
+    o = OPTS["momentum_damp_wd"]
+    st, coef = _setup("feddyn", o, P, 21, prebuf=True)
+    step, d = _step_for(st, coef, "feddyn", o, dev, want_avg=True)
+    avg = ref.reduce(X, w, W=sum(w))
+    st.step(avg)
+    agg.pop_step("local_params", step)
+    assert "local_params" not in agg
+    _check(st, avg, d, "feddyn", o)
+
+
+def test_optimize_takes_the_fused_path(dev, monkeypatch):
+    """FedAvg.optimize with plain SGD on a fresh round never calls the
+    standalone step kernel: pop and step run as one reduction pass."""
+    from fedsim_amd import ops
+    from fedsim_amd.distributed.centralized.training import FedAvg
+    from fedsim_amd.utils import SerialAggregator, Storage
+
+    K, P = 6, 5_003
+    X = V.client_rows("realistic", K, P, 4)
+    w = V.client_weights("fedavg", K, 4)
+    agg = SerialAggregator()
+    for k in range(K):
+        agg.add("local_params", torch.from_numpy(X[k].copy()).to(dev), w[k])
+
+    def boom(self, avg):
+        raise AssertionError("unfused step called")
+
+    monkeypatch.setattr(ops.ServerStep, "apply", boom)
+    cloud0 = V.cloud_vector(P, 5)
+    cloud = torch.from_numpy(cloud0.copy()).to(dev).requires_grad_(True)
+    st = Storage()
+    st.write("cloud_params", cloud)
+    st.write("optimizer", torch.optim.SGD(params=[cloud], lr=0.3))
+    st.write("lr_scheduler", None)
+    FedAvg.optimize(st, agg, None)
+    exp = ref.fedavg_sgd(ref.reduce(X, w, W=sum(w)), cloud0, 0.3)
+    np.testing.assert_array_equal(bits(cloud.detach().cpu().numpy()), bits(exp))

@@ -44,16 +44,32 @@ def timed(fn, steps, warmup=2):
     return (time.perf_counter() - t0) / steps
 
 
-def round_exact(Xb, w32, W, P, epilogue=None, pool_passes=1, K_pool=None):
-    avg = torch.empty(P, device=Xb.device)
-    cloud = torch.zeros(P, device=Xb.device)
-    prev = torch.zeros(P, device=Xb.device)
+def round_exact(Xb, w32, W, P, epilogue=None, pool_passes=1, K_pool=None, fused=False):
+    """One round: pool_passes reduce passes (+ divide in the last), then the
+    server step.  fused=True runs the step inside the last pass
+    (fedagg_reduce_step_blocked_f32, what <Algo>.optimize does), writing the
+    pseudo-gradient too as the product path does."""
+    dev = Xb.device
+    avg = torch.empty(P, device=dev)
+    cloud = torch.zeros(P, device=dev)
+    prev = torch.zeros(P, device=dev)
+    grad = torch.empty(P, device=dev)
+    step = None
+    if fused and epilogue:
+        step = ops.ServerStep(epilogue, cloud, lr=1.0, coef=0.6 if epilogue == "adabest" else 0.0,
+                              aux=prev if epilogue == "adabest" else None, grad_out=grad)
 
     def fn():
         for i in range(pool_passes):
             last = i == pool_passes - 1
+            if last and step is not None:
+                ops.reduce_blocked_step(Xb, w32, step, B=K_pool,
+                                        acc_in=None if i == 0 else avg, W=W)
+                continue
             ops.reduce_blocked(Xb, w32, avg, B=K_pool, acc_in=None if i == 0 else avg,
                                W=W if last else None, flags=ops.default_flags(Xb.shape[2]))
+        if step is not None:
+            return avg
         if epilogue == "fedavg":
             ops.fedavg_sgd(avg, cloud, 1.0)
         elif epilogue == "adabest":
@@ -101,8 +117,11 @@ def main():
         Xb = blocked_random(K, P, dev, 1)
         ws = [1] * K if epi == "adabest" else [int(v) for v in rng.integers(50, 601, size=K)]
         w32 = torch.tensor([ops.fl32(v) for v in ws], device=dev)
-        fn, _ = round_exact(Xb, w32, sum(ws), P, epilogue=epi)
-        report(name, K, P, timed(fn, max(a.steps, 20)), dict(epilogue=epi))
+        for fused in (True, False):
+            fn, _ = round_exact(Xb, w32, sum(ws), P, epilogue=epi, fused=fused)
+            report(name + ("" if fused else "_split"), K, P, timed(fn, max(a.steps, 20)),
+                   dict(epilogue=epi, step="fused into the last reduce" if fused
+                        else "separate epilogue launch"))
         del Xb
 
     if "cfg4" in only:
@@ -110,7 +129,7 @@ def main():
         Xb = blocked_random(K, P, dev, 2 + rank)
         ws = [int(v) for v in rng.integers(50, 601, size=K)]
         w32 = torch.tensor([ops.fl32(v) for v in ws], device=dev)
-        fn, _ = round_exact(Xb, w32, sum(ws), P, epilogue="fedavg")
+        fn, _ = round_exact(Xb, w32, sum(ws), P, epilogue="fedavg", fused=True)
         if dist is not None:
             dist.barrier()
         report("cfg4_param_shard", K, P, timed(fn, a.steps),

@@ -13,7 +13,7 @@ timeout -k 10 300 ./tools/hbm_peak 32 > "$OUT/hbm_peak.json" 2> "$OUT/hbm_peak.e
 && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write \
      -- python bench.py $ARGS > "$OUT/pmc_write.log" 2>&1 \
 && python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --K 1000 --P 25000000 \
-     --flags 260 --layout blocked4096 --out "$OUT/pmc_traffic.json"
+     --flags 260 --layout blocked4096 --step fused --out "$OUT/pmc_traffic.json"
 rc=$?
 echo "exit $rc"
 exit $rc

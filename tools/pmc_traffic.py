@@ -7,6 +7,10 @@ of the reduce kernel, with the gfx950 corrections from MI355X_MICROARCH.md §HBM
 Writes profiles/pmc_traffic.json, read by bench.py for roofline.traffic.
 
 usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR --K 1000 --P 25000000 --flags N
+           [--step fused|split]
+  fused: the reduce kernel with the server-step epilogue (EpiStep): algorithmic
+         bytes 4KP + 4K + 12P (rows, weights, cloud read + write, grad write)
+  split: the plain reduce (EpiStore): 4KP + 4K + 4P (the average's write)
 """
 import argparse
 import csv
@@ -17,7 +21,7 @@ import os
 KERNEL = "k_reduce_vec"
 
 
-def read_counter(d, name):
+def read_counter(d, name, tag):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -25,7 +29,8 @@ def read_counter(d, name):
     for fn in files:
         with open(fn) as f:
             for row in csv.DictReader(f):
-                if KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == name:
+                kn = row.get("Kernel_Name", "")
+                if KERNEL in kn and tag in kn and row.get("Counter_Name") == name:
                     vals.append(float(row["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {name} rows for {KERNEL} in {files}")
@@ -40,18 +45,20 @@ def main():
     ap.add_argument("--P", type=int, required=True)
     ap.add_argument("--flags", type=int, required=True)
     ap.add_argument("--layout", default="blocked4096", help="strided | blocked<C>")
+    ap.add_argument("--step", default="fused", choices=["fused", "split"])
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                   "pmc_traffic.json"))
     a = ap.parse_args()
-    fetch = read_counter(a.fetch_dir, "FETCH_SIZE")
-    write = read_counter(a.write_dir, "WRITE_SIZE")
+    tag = "EpiStep" if a.step == "fused" else "EpiStore"
+    fetch = read_counter(a.fetch_dir, "FETCH_SIZE", tag)
+    write = read_counter(a.write_dir, "WRITE_SIZE", tag)
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
     fetch_b = f_kib * 1024 * 2
     write_b = w_kib * 1024
-    alg = 4.0 * a.K * a.P + 4.0 * a.P + 4.0 * a.K
+    alg = 4.0 * a.K * a.P + 4.0 * a.K + (12.0 if a.step == "fused" else 4.0) * a.P
     out = dict(
-        kernel=KERNEL, K=a.K, P=a.P, flags=a.flags, layout=a.layout,
+        kernel=f"{KERNEL} ({tag})", K=a.K, P=a.P, flags=a.flags, layout=a.layout, step=a.step,
         dispatches=dict(fetch=len(fetch), write=len(write)),
         FETCH_SIZE_KiB_mean=f_kib, WRITE_SIZE_KiB_mean=w_kib,
         fetch_bytes_corrected=fetch_b, write_bytes=write_b,
