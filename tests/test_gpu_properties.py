@@ -1,0 +1,149 @@
+"""Property-based GPU parity (hypothesis): random client counts, sizes, value
+ranges, weight kinds, column-block widths, slab capacities and ring splits,
+every layout and the fused pop + step, against the C oracle.
+
+Bar: bit-exact for finite results.  Where an input overflow makes inf - inf,
+both sides produce a NaN, but its sign/payload is not pinned (x86's default
+NaN is negative, CDNA's is positive). Those positions are compared as "NaN
+on both sides", and every other position bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from conftest import bits
+from oracle import ref
+from test_oracle_properties import rounds
+
+pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore::RuntimeWarning")]
+
+SETTINGS = settings(max_examples=60, deadline=None, derandomize=True,
+                    suppress_health_check=[HealthCheck.too_slow,
+                                           HealthCheck.function_scoped_fixture])
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from fedsim_amd import _native
+
+    _native.load()
+    return torch.device("cuda:0")
+
+
+def same(got, exp):
+    got = np.asarray(got, dtype=np.float32)
+    nan_g, nan_e = np.isnan(got), np.isnan(exp)
+    np.testing.assert_array_equal(nan_g, nan_e)
+    np.testing.assert_array_equal(bits(got[~nan_g]), bits(exp[~nan_e]))
+
+
+def _accepted(X, w):
+    keep = [k for k in range(len(w)) if w[k] > 0]
+    return X[keep], [w[k] for k in keep]
+
+
+@SETTINGS
+@given(rounds(max_k=40, max_p=9000), st.sampled_from([1024, 2048, 4096]),
+       st.integers(0, 5), st.data())
+def test_blocked_ring_random(dev, r, C, pad, data):
+    from fedsim_amd import ops
+
+    X, w = r
+    Xa, wa = _accepted(X, w)
+    B, P = len(wa), X.shape[1]
+    if B == 0:
+        return
+    W = sum(wa)
+    Xb = ops.to_blocked(torch.from_numpy(Xa).to(dev), C, kcap=B + pad)
+    w32 = torch.tensor([ops.fl32(v) for v in wa], dtype=torch.float32, device=dev)
+    out = torch.empty(P, device=dev)
+    cut = data.draw(st.integers(0, B))
+    if cut:
+        ops.reduce_blocked(Xb, w32[:cut].contiguous(), out, B=cut)
+    ops.reduce_blocked(Xb, w32[cut:].contiguous(), out, B=B - cut,
+                       acc_in=out if cut else None, W=W, r0=cut)
+    exp = ref.reduce(Xa, wa, W=W)
+    same(out.cpu().numpy(), exp)
+
+
+@SETTINGS
+@given(rounds(max_k=20, max_p=5000), st.sampled_from(["fedavg", "adabest", "feddyn"]),
+       st.sampled_from([0.0, 0.9]), st.floats(0.05, 1.5))
+def test_fused_step_random(dev, r, algo, m, lr):
+    from fedsim_amd import ops
+
+    X, w = r
+    Xa, wa = _accepted(X, w)
+    B, P = len(wa), X.shape[1]
+    if B == 0:
+        return
+    W = sum(wa)
+    avg = ref.reduce(Xa, wa, W=W)
+    rng = np.random.default_rng(P + B)
+    cloud0 = rng.normal(0, 0.05, P).astype(np.float32)
+    aux0 = rng.normal(0, 0.05, P).astype(np.float32) if algo != "fedavg" else None
+    s = ref.ServerState(algo, cloud0, dict(lr=lr, momentum=m), aux=aux0, coef=0.6)
+    s.step(avg)
+    cloud = torch.from_numpy(cloud0.copy()).to(dev)
+    aux = torch.from_numpy(aux0.copy()).to(dev) if aux0 is not None else None
+    buf = torch.empty(P, device=dev) if m else None
+    grad = torch.empty(P, device=dev)
+    step = ops.ServerStep(algo, cloud, lr=lr, momentum=m, coef=0.6, aux=aux, momentum_buf=buf,
+                          momentum_init=bool(m), grad_out=grad)
+    C = ops.choose_block_cols(P)
+    Xb = ops.to_blocked(torch.from_numpy(Xa).to(dev), C)
+    w32 = torch.tensor([ops.fl32(v) for v in wa], dtype=torch.float32, device=dev)
+    ops.reduce_blocked_step(Xb, w32, step, W=W)
+    same(cloud.cpu().numpy(), s.cloud)
+    same(grad.cpu().numpy(), s.grad)
+    if aux is not None:
+        same(aux.cpu().numpy(), s.aux)
+    if m:
+        same(buf.cpu().numpy(), s.buf)
+
+
+@SETTINGS
+@given(rounds(max_k=24, max_p=3000), st.integers(1, 9))
+def test_aggregator_random_stream(dev, r, max_rows):
+    """add() x K through a small ring (host and HBM sources), then pop()."""
+    from fedsim_amd.utils import SerialAggregator
+
+    X, w = r
+    agg = SerialAggregator(max_rows=max_rows)
+    for k in range(X.shape[0]):
+        src = torch.from_numpy(X[k].copy())
+        agg.add("p", src.to(dev) if k % 2 else src, w[k])
+    if X.shape[0] == 0:
+        assert "p" not in agg
+        return
+    got = agg.pop("p")
+    W = sum(w)  # add() does not skip zero weights; W == 0 -> pop returns the raw sum
+    same(got.cpu().numpy(), ref.reduce(X, w, W=W if W else None))
+
+
+@pytest.mark.parametrize("C", [1024, 4096])
+def test_nonfinite_inputs(dev, C):
+    """+-inf and NaN client values (a diverged client the caller did not flag)
+    propagate as in the reference: inf stays inf with its sign, inf - inf and
+    NaN inputs give NaN at exactly the same positions."""
+    from fedsim_amd import ops
+
+    K, P = 6, 5000
+    rng = np.random.default_rng(17)
+    X = rng.standard_normal((K, P)).astype(np.float32)
+    X[0, :100] = np.inf
+    X[1, 50:150] = -np.inf          # inf - inf in columns 50..99
+    X[2, 200:220] = np.nan
+    X[3, 300:310] = np.float32(3e38)  # overflows to inf once weighted
+    w = [3, 1, 2, 7, 5, 4]
+    W = sum(w)
+    Xb = ops.to_blocked(torch.from_numpy(X).to(dev), C)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    out = torch.empty(P, device=dev)
+    ops.reduce_blocked(Xb, w32, out, W=W)
+    exp = ref.reduce(X, w, W=W)
+    assert np.isnan(exp[50:100]).all() and np.isposinf(exp[:50]).all()
+    same(out.cpu().numpy(), exp)
