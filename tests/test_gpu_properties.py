@@ -19,7 +19,7 @@ from test_oracle_properties import rounds
 
 pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore::RuntimeWarning")]
 
-SETTINGS = settings(max_examples=60, deadline=None, derandomize=True,
+SETTINGS = settings(max_examples=250, deadline=None, derandomize=True,
                     suppress_health_check=[HealthCheck.too_slow,
                                            HealthCheck.function_scoped_fixture])
 
