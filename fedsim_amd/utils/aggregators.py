@@ -450,8 +450,9 @@ class AppendixAggregator(object):
     def get(self, key, k=None):
         self._check(key)
         list_v, list_w, _ = (list(x) for x in self._members[key])
+        # the reference slices [-min(k, n):], so k=0 (a -0 slice) means "all"
         n = len(list_v) if k is None else min(k, len(list_v))
-        vs, ws = list_v[len(list_v) - n:], list_w[len(list_w) - n:]
+        vs, ws = list_v[-n:], list_w[-n:]
         return sum(v * w for v, w in zip(vs, ws)) / sum(ws)
 
     def get_values(self, key):
@@ -473,27 +474,6 @@ class AppendixAggregator(object):
         self._check(key)
         list_v, list_w, _ = self._members.pop(key)
         return sum(v * w for v, w in zip(list_v, list_w)) / sum(list_w)
-
-    def device_of(self, key) -> Optional[torch.device]:
-        """HIP device holding a tensor key's sum (None for host keys)."""
-        e = self._entry(key)
-        return e.dev if isinstance(e, _DeviceEntry) else None
-
-    def pop_step(self, key, step: ops.ServerStep) -> None:
-        """``pop(key)`` and ``step.apply(average)`` in one pass over the
-        pending client rows (not part of the reference API): the server step
-        of FedAvg / AdaBest / FedNova / FedDyn optimize runs in the epilogue of
-        the round's last reduction, so the average is never stored."""
-        e = self._entry(key)
-        if not isinstance(e, _DeviceEntry):
-            avg = self.pop(key)
-            step.apply(avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
-            return
-        del self._members[key]
-        if e.dev != step.cloud.device:
-            step.apply(e.pop(on_device=True).reshape(-1).to(step.cloud.device))
-            return
-        e.pop_step(step)
 
     def items(self):
         for key in self._members.keys():

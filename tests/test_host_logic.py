@@ -126,7 +126,12 @@ def test_appendix_aggregator():
     a.append("s", 4.0, weight=1, step=2)  # evicts the first entry
     assert a.get("s") == (2.0 * 3 + 4.0) / 4
     assert a.get("s", k=1) == 4.0
+    # reference quirk (aggregators.py:211-215): k=0 slices [-0:], i.e. everything
+    assert a.get("s", k=0) == a.get("s") == a.get("s", k=99)
     assert list(a.get_steps("s")) == [1, 2]
+    assert not hasattr(a, "pop_step")
+    with pytest.raises(Exception, match="is not in the aggregator"):
+        a.get("missing")
     a.append_all({"t": 5.0}, step=3)
     assert a.pop_all() == {"s": (2.0 * 3 + 4.0) / 4, "t": 5.0}
 

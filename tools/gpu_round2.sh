@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r01d}
 mkdir -p "$OUT"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
 && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
 && timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
 && timeout -k 10 600 python tools/bench_configs.py > "$OUT/configs.jsonl" 2> "$OUT/configs.err" \
