@@ -1,0 +1,140 @@
+"""FedDF (ensemble distillation) on the MI355X aggregation path.
+
+Reference: fedsim/distributed/centralized/training/feddf.py:19-142.  Per round:
+the client vectors are averaged like FedAvg (``pop``, here the exact HIP
+reduction) and the average becomes the cloud model (feddf.py:97-99); then, for
+every batch of the server's distillation split, the K client models are run
+as teachers, their logits averaged through a SerialAggregator with weight 1
+(feddf.py:117-122), and the cloud model takes one server-optimizer step on the
+KL divergence to that average (feddf.py:124-140).
+
+MI355X-first differences (same results):
+
+* The reference re-copies every teacher into the model for every batch
+  (``initialize_module``, K x P bytes per batch).  Here the K teacher vectors
+  are stacked once per round into one [K, P] HBM slab and each teacher runs
+  through ``functional_call`` on views of its row.
+* On a HIP device, and for models without buffers, the K teacher forwards run
+  as ONE batched forward (``torch.func.vmap`` over the slab rows, chunked to
+  bound activation memory) into a [K, B*C] logits slab, and the teacher
+  average is one launch of the exact-mode reduce kernel
+  (``fedagg_reduce_f32``, weights 1, divide by fl32(K)): the same per-element
+  arithmetic and order as the reference's ``add(target, 1)`` x K + ``get``.
+* Elsewhere (host-resident model, or a model with buffers such as BatchNorm,
+  whose running statistics cannot be updated under vmap) the teachers run one
+  after another, as in the reference, and their logits go through the
+  device-backed SerialAggregator.  With ``device="cpu"`` every forward is
+  then the reference's own CPU arithmetic and the whole round is bitwise
+  equal to it (tests/test_gpu_roundloop.py).
+"""
+from __future__ import annotations
+
+import torch
+from torch.func import functional_call
+from torch.nn.functional import log_softmax
+
+from .... import ops
+from ....scores import KLDivScore
+from ....utils import SerialAggregator, initialize_module, vector_to_named_parameters_like
+from .fedavg import FedAvg
+from .utils import serial_aggregation
+
+_TEACHER_CHUNK = 64  # teachers per batched forward (bounds activation memory)
+
+
+class TeacherEnsemble(object):
+    """K teacher parameter vectors stacked in one slab; ``mean_logits(x)`` is
+    the reference's weight-1 SerialAggregator average of their outputs."""
+
+    def __init__(self, model, teacher_vectors, device):
+        self.model = model
+        self.named = list(model.named_parameters())
+        self.slab = torch.stack([t.reshape(-1) for t in teacher_vectors]).to(device)
+        self.K = self.slab.shape[0]
+        self.batched = (self.slab.device.type == "cuda"
+                        and len(list(model.buffers())) == 0)
+        self._w32 = None
+
+    def _forward(self, flat, x):
+        return functional_call(self.model, vector_to_named_parameters_like(flat, self.named), (x,))
+
+    @torch.no_grad()
+    def mean_logits(self, x):
+        if not self.batched:
+            agg = SerialAggregator()
+            for k in range(self.K):
+                agg.add("target", self._forward(self.slab[k], x).clone(), 1)
+            return agg.get("target")
+        chunks = []
+        for k0 in range(0, self.K, _TEACHER_CHUNK):
+            part = self.slab[k0:k0 + _TEACHER_CHUNK]
+            chunks.append(torch.vmap(self._forward, in_dims=(0, None))(part, x))
+        logits = torch.cat(chunks) if len(chunks) > 1 else chunks[0]
+        K, shape = logits.shape[0], logits.shape[1:]
+        rows = logits.reshape(K, -1).float().contiguous()
+        if self._w32 is None:
+            self._w32 = torch.ones(K, dtype=torch.float32, device=rows.device)
+        out = torch.empty(rows.shape[1], dtype=torch.float32, device=rows.device)
+        ops.reduce_slab(rows, self._w32, out, W=K)
+        return out.view(shape)
+
+    def load_last(self):
+        """Leave the model holding the last teacher, as the reference's
+        per-teacher initialize_module does (feddf.py:119)."""
+        initialize_module(self.model, self.slab[-1])
+
+
+class FedDF(FedAvg):
+    def init(server_storage, *args, **kwrag):
+        default_global_train_split = "valid"
+        default_global_epochs = 1
+        FedAvg.init(server_storage)
+        server_storage.write("global_train_split",
+                             kwrag.get("global_train_split", default_global_train_split))
+        server_storage.write("global_epochs", kwrag.get("global_epochs", default_global_epochs))
+
+    def receive_from_client(server_storage, client_id, client_msg, train_split_name,
+                            serial_aggregator, appendix_aggregator):
+        params = client_msg["local_params"].clone().detach().data
+        appendix_aggregator.append("local_params", params)
+        return serial_aggregation(server_storage, client_id, client_msg, train_split_name,
+                                  serial_aggregator)
+
+    def optimize(server_storage, serial_aggregator, appendix_aggregator):
+        if "local_params" in serial_aggregator:
+            param_avg = serial_aggregator.pop("local_params")
+            cloud_params = server_storage.read("cloud_params")
+            cloud_params.data = param_avg.data
+
+            model = server_storage.read("model")
+            global_train_split = server_storage.read("global_train_split")
+            train_data_loader = server_storage.read("global_dataloaders").get(global_train_split)
+            if train_data_loader is None:
+                raise Exception(f"no dataloader made for split {global_train_split} on the server!")
+            global_epochs = server_storage.read("global_epochs")
+            optimizer = server_storage.read("optimizer")
+            lr_scheduler = server_storage.read("lr_scheduler")
+            device = server_storage.read("device")
+
+            teachers = TeacherEnsemble(model, appendix_aggregator.get_values("local_params"),
+                                       device)
+            ran = False
+            for _ in range(global_epochs):
+                for x, _ in train_data_loader:
+                    x = x.to(device)
+                    target_out = log_softmax(teachers.mean_logits(x), 1)
+                    criterion = KLDivScore(log_target=True)
+                    param_dict = vector_to_named_parameters_like(cloud_params,
+                                                                 model.named_parameters())
+                    pred = functional_call(model, param_dict, x)
+                    pred_out = log_softmax(pred, 1)
+                    loss = criterion(pred_out, target_out.data)
+                    optimizer.zero_grad()
+                    loss.backward()
+                    optimizer.step()
+                    if lr_scheduler is not None:
+                        lr_scheduler.step()
+                    ran = True
+            if ran:
+                teachers.load_last()
+        return serial_aggregator.pop_all()

@@ -7,6 +7,8 @@ autograd; nothing here is a HIP kernel of this project.
 """
 from __future__ import annotations
 
+import inspect
+
 import torch
 from torch.nn.utils import clip_grad_norm_
 
@@ -34,6 +36,20 @@ def default_step_closure(x, y, model, criterion, optimizer, scores, max_grad_nor
     return loss
 
 
+def _scheduler_step(lr_scheduler, scores, criterion):
+    """training.py:90-105: a scheduler whose step takes ``metrics`` (e.g.
+    ReduceLROnPlateau) is fed the score named by its ``trigger_metric``."""
+    if "metrics" in inspect.signature(lr_scheduler.step).parameters:
+        comb_scores = {**scores, **{criterion.get_name(): criterion}}
+        trigger_metric = lr_scheduler.trigger_metric
+        if trigger_metric not in comb_scores:
+            raise Exception(f"{trigger_metric} not in local scores. "
+                            f"Possible options are {comb_scores.keys()}")
+        lr_scheduler.step(comb_scores[trigger_metric].get_score())
+    else:
+        lr_scheduler.step()
+
+
 def local_train(model, train_data_loader, epochs, steps, criterion, optimizer,
                 lr_scheduler=None, device="cpu", step_closure=default_step_closure,
                 scores=None, max_grad_norm=1000, **step_ctx):
@@ -54,7 +70,7 @@ def local_train(model, train_data_loader, epochs, steps, criterion, optimizer,
                 num_steps += 1
                 num_train_samples += y.shape[0]
                 if lr_scheduler is not None:
-                    lr_scheduler.step()
+                    _scheduler_step(lr_scheduler, scores, criterion)
     return num_train_samples, num_steps, diverged
 
 

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 from torch import nn
 from torch.nn.utils import parameters_to_vector
+from torch.utils.data import TensorDataset
 
 from . import vectors as V
 
@@ -39,6 +40,28 @@ class FakeDataManager(object):
 
     def get_local_splits_names(self):
         return ["train"]
+
+
+class TensorDataManager(FakeDataManager):
+    """FakeDataManager with real (x, y) data, for runs that keep the
+    algorithm's own send_to_server (local SGD on the client) and for FedDF's
+    server-side distillation split ("valid", feddf.py:66-78)."""
+
+    def __init__(self, num_clients=NUM_CLIENTS, valid_size=0):
+        super().__init__(num_clients)
+        self.valid_size = valid_size
+
+    @staticmethod
+    def _data(seed, n):
+        x = torch.from_numpy(V.gauss(seed, n * 37).astype(np.float32).reshape(n, 37))
+        y = torch.from_numpy(V.randint(seed + 1, n, 0, 2))
+        return TensorDataset(x, y)
+
+    def get_global_dataset(self):
+        return {"valid": self._data(90001, self.valid_size)} if self.valid_size else {}
+
+    def get_local_dataset(self, client_id):
+        return {"train": self._data(1000 + 2 * client_id, self.sizes[client_id])}
 
 
 class TinyModel(nn.Module):

@@ -1,0 +1,96 @@
+"""Client side (the producer of the aggregated vectors), on CPU: one client's
+``send_to_server`` — local SGD through local_train / default_step_closure and
+the CrossEntropyScore criterion, FedProx's proximal gradient term — reproduces
+the reference's own output bit for bit (tests/golden/rounds.json "clients",
+made by tools/gen_golden_rounds.py from fedprox.py:68-127 / fedavg.py:88-179)."""
+import json
+import os
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN_DIR, bits
+from oracle import synthetic_fl as S
+
+with open(os.path.join(GOLDEN_DIR, "rounds.json")) as _f:
+    CLIENTS = json.load(_f)["clients"]
+
+
+@pytest.fixture(scope="module")
+def arrays():
+    with np.load(os.path.join(GOLDEN_DIR, "rounds.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("case", CLIENTS, ids=[c["id"] for c in CLIENTS])
+def test_send_to_server_matches_reference(case, arrays):
+    from fedsim_amd import scores
+    from fedsim_amd.distributed.centralized import training
+
+    cls = getattr(training, case["algorithm"])
+    lopt = case["local_opt"]
+    torch.manual_seed(S.TORCH_SEED)
+    dm = S.TensorDataManager()
+    alg = cls(data_manager=dm, metric_logger=None, num_clients=S.NUM_CLIENTS,
+              sample_scheme="uniform", sample_rate=S.SAMPLE_RATE, model_def=S.TinyModel,
+              epochs=2, criterion_def="CrossEntropyScore",
+              local_optimizer_def=partial(torch.optim.SGD, **lopt), device="cpu",
+              **case["alg_kwargs"])
+    st = alg.get_server_storage()
+    cid = case["client_id"]
+    ctx = cls.send_to_client(st, cid)
+    torch.manual_seed(1000 + cid)
+    msg = cls.send_to_server(cid, case["rounds"], None, dm.get_local_dataset(cid), "train", {},
+                             2, scores.CrossEntropyScore(), 32, 64,
+                             partial(torch.optim.SGD, **lopt), None, "cpu", ctx=ctx)
+    np.testing.assert_array_equal(bits(msg["local_params"].numpy()),
+                                  bits(arrays[f"{case['id']}/local_params"]))
+    assert msg["num_steps"] == case["num_steps"]
+    assert msg["diverged"] == case["diverged"]
+    assert msg["num_samples"] == case["num_samples"]
+    assert msg["metrics"] == case["metrics"]
+
+
+def test_fedprox_server_side_is_fedavg():
+    """fedprox.py:16 inherits FedAvg's receive_from_client / optimize, so a
+    --algorithm FedProx round runs the same fused server kernel."""
+    from fedsim_amd.distributed.centralized.training import FedAvg, FedProx
+
+    for name in ("receive_from_client", "optimize", "deploy", "report"):
+        assert getattr(FedProx, name) is getattr(FedAvg, name)
+
+
+def test_scores_match_reference_arithmetic():
+    """scores.py:180-346: sum-reduced loss / batch; micro vs macro running
+    means; KL with log targets; Accuracy hits."""
+    from fedsim_amd import scores
+
+    g = torch.Generator().manual_seed(0)
+    logits = torch.randn(7, 5, generator=g)
+    y = torch.randint(0, 5, (7,), generator=g)
+    ce = scores.CrossEntropyScore()
+    v = ce(logits, y)
+    ref = torch.nn.CrossEntropyLoss(reduction="sum")(logits, y) / 7
+    assert bits(v.numpy()) == bits(ref.numpy())
+    ce(logits[:3], y[:3])
+    s3 = torch.nn.CrossEntropyLoss(reduction="sum")(logits[:3], y[:3]).item()
+    s7 = torch.nn.CrossEntropyLoss(reduction="sum")(logits, y).item()
+    assert ce.get_score() == (s7 + s3) / 10
+    mac = scores.CrossEntropyScore(reduction="macro")
+    mac(logits, y)
+    mac(logits[:3], y[:3])
+    assert mac.get_score() == (s7 / 7 + s3 / 3) / 2
+    acc = scores.Accuracy()
+    acc(logits, y)
+    assert acc.get_score() == (logits.argmax(1) == y).sum().item() / 7
+    kl = scores.KLDivScore(log_target=True)
+    lp, lq = torch.log_softmax(logits, 1), torch.log_softmax(logits.flip(0), 1)
+    assert bits(kl(lp, lq).numpy()) == bits(
+        (torch.nn.KLDivLoss(log_target=True, reduction="sum")(lp, lq) / 7).numpy())
+    with pytest.raises(Exception, match="size mismatch"):
+        ce(logits, y[:3])
+    with pytest.raises(Exception, match="invalid log_freq"):
+        scores.Accuracy(log_freq=0)
+    assert scores.Score().get_score() == 0
