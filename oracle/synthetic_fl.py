@@ -96,3 +96,20 @@ def make_algorithm(base_cls):
     """Subclass of an algorithm class with the synthetic client side."""
     return type("Synthetic" + base_cls.__name__, (base_cls,),
                 {"send_to_server": synthetic_send_to_server})
+
+
+def host_signature():
+    """CPU model + torch's CPU kernel capability.  Dense CPU math (local SGD's
+    GEMMs) rounds differently on another CPU (MKL/oneDNN pick per-ISA and
+    per-vendor kernels), so runs with local training are bit-reproducible only
+    on a host with the same signature as the one that made the goldens."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{model} | {torch.backends.cpu.get_cpu_capability()}"

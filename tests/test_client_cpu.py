@@ -1,7 +1,8 @@
 """Client side (the producer of the aggregated vectors), on CPU: one client's
 ``send_to_server`` — local SGD through local_train / default_step_closure and
 the CrossEntropyScore criterion, FedProx's proximal gradient term — reproduces
-the reference's own output bit for bit (tests/golden/rounds.json "clients",
+the reference's own output bit for bit on the goldens' CPU, within 1e-5
+normwise on another (tests/golden/rounds.json "clients",
 made by tools/gen_golden_rounds.py from fedprox.py:68-127 / fedavg.py:88-179)."""
 import json
 import os
@@ -15,7 +16,10 @@ from conftest import GOLDEN_DIR, bits
 from oracle import synthetic_fl as S
 
 with open(os.path.join(GOLDEN_DIR, "rounds.json")) as _f:
-    CLIENTS = json.load(_f)["clients"]
+    _G = json.load(_f)
+CLIENTS = _G["clients"]
+# bitwise on the goldens' own CPU; another CPU's GEMM kernels round differently
+SAME_HOST = _G.get("host") == S.host_signature()
 
 
 @pytest.fixture(scope="module")
@@ -45,12 +49,17 @@ def test_send_to_server_matches_reference(case, arrays):
     msg = cls.send_to_server(cid, case["rounds"], None, dm.get_local_dataset(cid), "train", {},
                              2, scores.CrossEntropyScore(), 32, 64,
                              partial(torch.optim.SGD, **lopt), None, "cpu", ctx=ctx)
-    np.testing.assert_array_equal(bits(msg["local_params"].numpy()),
-                                  bits(arrays[f"{case['id']}/local_params"]))
+    got, want = msg["local_params"].numpy(), arrays[f"{case['id']}/local_params"]
     assert msg["num_steps"] == case["num_steps"]
     assert msg["diverged"] == case["diverged"]
     assert msg["num_samples"] == case["num_samples"]
-    assert msg["metrics"] == case["metrics"]
+    if SAME_HOST:
+        np.testing.assert_array_equal(bits(got), bits(want))
+        assert msg["metrics"] == case["metrics"]
+    else:
+        assert np.linalg.norm(got.astype(np.float64) - want) <= 1e-5 * np.linalg.norm(want)
+        for k, v in case["metrics"]["train"].items():
+            assert msg["metrics"]["train"][k] == pytest.approx(v, rel=1e-5)
 
 
 def test_fedprox_server_side_is_fedavg():

@@ -9,11 +9,13 @@ the host, every aggregation on the MI355X), and device="cuda" for the
 synthetic-client runs of the server-only algorithms (the cloud lives in HBM;
 the only arithmetic is the aggregation and server step, i.e. our kernels).
 
-Runs that also do dense model math on the GPU — local SGD of real clients, or
-FedDF's teacher / distillation forwards — use rocBLAS/MIOpen kernels whose
-rounding differs from the CPU's, so on device="cuda" they are held to a
-normwise tolerance instead: ||cloud - golden|| <= 1e-4 ||golden|| after 5
-rounds, and the score report within 1e-4 relative."""
+Runs that also do dense model math — local SGD of real clients, or FedDF's
+teacher / distillation forwards — are bitwise only on device="cpu" on a host
+whose CPU matches the one that made the goldens (oracle/synthetic_fl.py
+host_signature: MKL/oneDNN GEMMs round per ISA and vendor).  On the GPU
+(rocBLAS/MIOpen) or another CPU they are held to a normwise tolerance:
+||cloud - golden|| <= 1e-4 ||golden|| after 5 rounds, and the score report
+within 1e-4 relative."""
 import json
 import os
 import random
@@ -29,7 +31,9 @@ from oracle import synthetic_fl as S
 pytestmark = pytest.mark.gpu
 
 with open(os.path.join(GOLDEN_DIR, "rounds.json")) as _f:
-    RUNS = json.load(_f)["runs"]
+    _G = json.load(_f)
+RUNS = _G["runs"]
+SAME_HOST = _G.get("host") == S.host_signature()
 
 RTOL = 1e-4
 
@@ -41,8 +45,8 @@ def arrays():
 
 
 def _bitwise(run, device):
-    dense_on_gpu = run.get("client") == "local" or run["algorithm"] == "FedDF"
-    return device == "cpu" or not dense_on_gpu
+    dense = run.get("client") == "local" or run["algorithm"] == "FedDF"
+    return not dense or (device == "cpu" and SAME_HOST)
 
 
 def _make(run, device):

@@ -128,8 +128,8 @@ def main():
         print(rid, name, akw, meta["num_steps"], meta["metrics"])
     gd = os.path.join(REPO, "tests", "golden")
     with open(os.path.join(gd, "rounds.json"), "w") as f:
-        json.dump(dict(generator="tools/gen_golden_rounds.py", runs=manifest, clients=clients),
-                  f, indent=1)
+        json.dump(dict(generator="tools/gen_golden_rounds.py", host=S.host_signature(),
+                       runs=manifest, clients=clients), f, indent=1)
     np.savez_compressed(os.path.join(gd, "rounds.npz"), **arrays)
 
 
