@@ -124,6 +124,11 @@ SIGNATURES = {
          ctypes.c_int64, ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
          ctypes.POINTER(StepArgs), ctypes.c_void_p],
     ),
+    "fedagg_reduce_step_rows_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+         ctypes.c_float, ctypes.c_int, ctypes.POINTER(StepArgs), ctypes.c_void_p],
+    ),
     "fedagg_feddyn_sgd_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,

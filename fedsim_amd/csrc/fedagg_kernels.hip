@@ -938,6 +938,36 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
   return static_cast<int>(e);
 }
 
+int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_t B,
+                                int64_t P, const float* acc_in, float W32, int flags,
+                                const fedagg_step_args* step, void* stream) {
+  if (!step) return FEDAGG_EINVAL;
+  StepPtrs sp;
+  bool mom;
+  int rc = make_step(step->algo, step->coef, step->cloud, step->aux, step->avg_prev,
+                     step->momentum_buf, step->momentum_init, step->grad_out, step->avg_out,
+                     &step->sgd, &sp, &mom);
+  if (rc != 0) return rc;
+  rc = check_reduce_args(w, B, P, acc_in, step->cloud, flags);
+  if (rc != 0 || P == 0) return rc;
+  if (flags & (FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
+  if (B > 0 && !rows) return FEDAGG_EINVAL;
+  if (!step_aligned(sp) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in))) return FEDAGG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const RowsTable tab{rows};
+  // the rows path's default configuration (256 lanes, 2 float4 slots per
+  // lane, U = 4); the rows are the caller's separate allocations
+  const bool nt = (flags & FEDAGG_NT) != 0;
+  hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+    return nt ? launch_vec<kBlock, kDefaultUnroll, 2, true, RowsTable, false>(
+                    tab, w, B, P, acc_in, epi, W32, flags, s)
+              : launch_vec<kBlock, kDefaultUnroll, 2, false, RowsTable, false>(
+                    tab, w, B, P, acc_in, epi, W32, flags, s);
+  });
+  if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
+  return static_cast<int>(e);
+}
+
 int fedagg_feddyn_sgd_f32(const float* avg, float ratio, float lr, float* cloud, float* h,
                           float* avg_prev, float* grad_out, int64_t P, void* stream) {
   if (P < 0) return FEDAGG_EINVAL;

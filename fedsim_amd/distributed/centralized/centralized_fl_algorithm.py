@@ -87,9 +87,11 @@ class CentralFLAlgorithm(object):
         }
         oracle_dataset = data_manager.get_oracle_dataset()
 
-        # size each round's HBM ring once for the clients it will receive
-        self._aggregator_factory = aggregator_factory or partial(SerialAggregator,
-                                                                 expected_rows=sample_count)
+        # size each round's HBM ring once for the clients it will receive, and
+        # reduce HBM-resident client vectors in place: a message is dropped
+        # right after receive_from_client, so its tensor can be handed over
+        self._aggregator_factory = aggregator_factory or partial(
+            SerialAggregator, expected_rows=sample_count, borrow=True)
         self._progress = progress
         self._server_memory = Storage()
         w = self._server_memory.write

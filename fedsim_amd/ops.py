@@ -162,8 +162,7 @@ def reduce_rows(
         if r.data_ptr() % 16:
             aligned = False
     if table is None:
-        host = torch.tensor([r.data_ptr() for r in rows] or [0], dtype=torch.int64)
-        table = host.to(out.device, non_blocking=False)
+        table = row_table(rows, out.device)
     f = flags
     if acc_in is None:
         f |= FEDAGG_INIT
@@ -440,6 +439,59 @@ def reduce_blocked_step(
         ctypes.byref(step.args), _stream_ptr(Xb.device),
     )
     check(rc, "fedagg_reduce_step_blocked_f32")
+    return step.cloud
+
+
+def row_table(rows: Sequence[torch.Tensor], device: torch.device) -> torch.Tensor:
+    """Device int64 table of the rows' data pointers (one pinned H2D copy,
+    stream-ordered on the current stream)."""
+    host = torch.tensor([r.data_ptr() for r in rows] or [0], dtype=torch.int64).pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def reduce_rows_step(
+    rows: Sequence[torch.Tensor],
+    w32: torch.Tensor,
+    step: ServerStep,
+    acc_in: Optional[torch.Tensor] = None,
+    W: Optional[float] = None,
+    nt: bool = True,
+    table: Optional[torch.Tensor] = None,
+) -> torch.Tensor:
+    """reduce_rows(rows, ..., out=avg) then step.apply(avg), fused into one
+    pass over the caller's own client tensors (fedagg_reduce_step_rows_f32):
+    the zero-copy round of HBM-resident client vectors.  Returns step.cloud."""
+    _require_hip_f32(w32, "w32")
+    P, dev = step.P, step.cloud.device
+    B = len(rows)
+    for i, r in enumerate(rows):
+        _require_hip_f32(r, f"rows[{i}]")
+        if r.numel() != P or not r.is_contiguous() or r.data_ptr() % 16:
+            raise ValueError(f"rows[{i}] must be contiguous, 16-B aligned, {P} elements")
+        if r.device != dev:
+            raise ValueError(f"rows[{i}] is on {r.device}, cloud on {dev}")
+    if w32.numel() < B:
+        raise ValueError("w32 too short")
+    if not step.aligned():
+        raise ValueError("every server-step operand must be 16-B aligned")
+    f = FEDAGG_NT if nt else 0
+    if acc_in is None:
+        f |= FEDAGG_INIT
+    else:
+        _require_hip_f32(acc_in, "acc_in")
+        if acc_in.numel() != P:
+            raise ValueError("acc_in size mismatch")
+    W32 = 0.0
+    if W is not None:
+        f |= FEDAGG_FINALIZE
+        W32 = fl32(W)
+    if table is None:
+        table = row_table(rows, dev)
+    rc = _native.load().fedagg_reduce_step_rows_f32(
+        table.data_ptr(), w32.data_ptr(), B, P, _ptr(acc_in), W32, f,
+        ctypes.byref(step.args), _stream_ptr(dev),
+    )
+    check(rc, "fedagg_reduce_step_rows_f32")
     return step.cloud
 
 

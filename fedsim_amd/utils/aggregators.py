@@ -117,15 +117,18 @@ class _Ingest(object):
 
 
 class _Options(object):
-    __slots__ = ("device", "slab_bytes", "max_rows", "flags", "expected_rows", "block_cols")
+    __slots__ = ("device", "slab_bytes", "max_rows", "flags", "expected_rows", "block_cols",
+                 "borrow")
 
-    def __init__(self, device, slab_bytes, max_rows, flags, expected_rows, block_cols):
+    def __init__(self, device, slab_bytes, max_rows, flags, expected_rows, block_cols,
+                 borrow=False):
         self.device = device
         self.slab_bytes = slab_bytes
         self.max_rows = max_rows
         self.flags = flags
         self.expected_rows = expected_rows
         self.block_cols = block_cols
+        self.borrow = borrow
 
 
 class _DeviceEntry(object):
@@ -140,7 +143,13 @@ class _DeviceEntry(object):
         self.C = opts.block_cols or ops.choose_block_cols(self.P)
         self.nblk = (self.P + self.C - 1) // self.C
         row_bytes = 4 * max(1, self.nblk) * self.C
-        self.Rmax = max(2, min(opts.max_rows, _slab_budget(dev, opts.slab_bytes) // row_bytes))
+        budget = _slab_budget(dev, opts.slab_bytes)
+        self.Rmax = max(2, min(opts.max_rows, budget // row_bytes))
+        # borrowed rows: HBM-resident client tensors reduced in place (no
+        # snapshot copy); at most Bmax are held before they are drained
+        self.borrow = opts.borrow
+        self.Bmax = max(1, min(opts.max_rows, budget // max(4, 4 * self.P)))
+        self.borrowed: List = []
         self.R = 0
         self.slab: Optional[torch.Tensor] = None
         self.hint = opts.expected_rows
@@ -188,9 +197,20 @@ class _DeviceEntry(object):
         if value.dtype != torch.float32:
             raise TypeError(f"device aggregation supports float32 tensors, got {value.dtype}")
         w32 = float(np.float32(weight))
+        src = value.detach().reshape(-1)
+        if self.borrow and self._borrowable(src):
+            if self.n_pending:
+                self._flush(final_W=None)  # earlier slab rows first: arrival order
+            elif len(self.borrowed) >= self.Bmax:
+                self._flush(final_W=None)
+            self.borrowed.append((src, src._version))
+            self.pending_w.append(w32)
+            self.cur_w = new_w
+            return
+        if self.borrowed:
+            self._flush(final_W=None)
         self._make_room()
         r = self.head
-        src = value.detach().reshape(-1)
         if src.device.type == "cuda":
             if src.device != self.dev:
                 src = src.to(self.dev)
@@ -204,11 +224,45 @@ class _DeviceEntry(object):
         self.pending_w.append(w32)
         self.cur_w = new_w
 
+    def _borrowable(self, src: torch.Tensor) -> bool:
+        return (src.device == self.dev and src.is_contiguous() and src.data_ptr() % 16 == 0
+                and src.numel() > 0)
+
+    def _flush_borrowed(self, final_W, step: Optional[ops.ServerStep] = None) -> None:
+        """Reduce the borrowed rows in place (pointer table, arrival order)."""
+        rows = []
+        for t, version in self.borrowed:
+            if t._version != version:
+                raise RuntimeError(
+                    "a client tensor was modified in place after SerialAggregator.add(); "
+                    "an aggregator created with borrow=True reads it when the round is "
+                    "reduced (use borrow=False to snapshot it at add time)")
+            rows.append(t)
+        cur = torch.cuda.current_stream(self.dev)
+        w32 = torch.tensor(self.pending_w, dtype=torch.float32).pin_memory()
+        w32 = w32.to(self.dev, non_blocking=True)
+        table = ops.row_table(rows, self.dev)
+        if step is not None:
+            ops.reduce_rows_step(rows, w32, step, acc_in=self.acc, W=final_W, table=table)
+        else:
+            acc_in = self.acc
+            if self.acc is None:
+                self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
+            ops.reduce_rows(rows, w32, self.acc, acc_in=acc_in, W=final_W,
+                            flags=ops.FEDAGG_NT, table=table)
+        for t in rows:  # the caller's allocations may belong to another stream
+            t.record_stream(cur)
+        self.borrowed = []
+        self.pending_w = []
+
     def _flush(self, final_W, step: Optional[ops.ServerStep] = None) -> None:
         """Reduce the pending rows into acc (arrival order); divide by
         fl32(final_W) in the same pass if given.  With ``step``, the last
         segment's pass also runs the server step on the result instead of
-        storing it (pop + optimize in one pass; needs n_pending > 0)."""
+        storing it (pop + optimize in one pass; needs pending rows)."""
+        if self.borrowed:
+            self._flush_borrowed(final_W, step)
+            return
         n = self.n_pending
         cur = torch.cuda.current_stream(self.dev)
         if n == 0:
@@ -274,7 +328,11 @@ class _DeviceEntry(object):
     def pop_step(self, step: ops.ServerStep) -> None:
         """pop(on_device=True) followed by step.apply(avg), fused into the last
         drain when rows are pending and the step's operands allow it."""
-        if self.n_pending == 0 or not ops.can_fuse_step(self.slab, step):
+        if self.borrowed:
+            fusable = step.aligned() and step.cloud.device == self.dev
+        else:
+            fusable = self.n_pending > 0 and ops.can_fuse_step(self.slab, step)
+        if not fusable:
             step.apply(self.pop(on_device=True).reshape(-1))
             return
         self._flush(final_W=self.cur_w if self._weighted() else None, step=step)
@@ -296,14 +354,22 @@ class SerialAggregator(object):
         expected_rows: hint (e.g. clients per round) to size the ring once.
         block_cols: column-block width C of the slab (1024 / 2048 / 4096);
             default = ops.choose_block_cols(P).
+        borrow: reduce HBM-resident client tensors where they are instead of
+            snapshotting them into the slab at ``add`` (no copy: the round
+            reads 4 B per client element instead of 12).  The caller hands the
+            tensor over: modifying it in place after ``add`` makes the next
+            reduction raise (torch's version counter is checked).  The round
+            driver enables it, since its client messages are dropped right
+            after ``receive_from_client``.
     """
 
     def __init__(self, device=None, slab_bytes: Optional[int] = _DEFAULT_SLAB_BYTES,
                  max_rows: int = _DEFAULT_MAX_ROWS, flags: Optional[int] = None,
                  expected_rows: Optional[int] = None,
-                 block_cols: Optional[int] = None) -> None:
+                 block_cols: Optional[int] = None, borrow: bool = False) -> None:
         self._members: Dict = dict()
-        self._opts = _Options(device, slab_bytes, max_rows, flags, expected_rows, block_cols)
+        self._opts = _Options(device, slab_bytes, max_rows, flags, expected_rows, block_cols,
+                              borrow)
         self._ingests: Dict = {}
 
     def _ingest(self, dev) -> _Ingest:

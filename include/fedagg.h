@@ -28,7 +28,7 @@
  *   fedagg_server_step_f32
  *       the three optimize epilogues above with any torch.optim.SGD
  *       configuration (momentum / nesterov / weight decay / maximize)
- *   fedagg_reduce_step_blocked_f32
+ *   fedagg_reduce_step_blocked_f32 / fedagg_reduce_step_rows_f32
  *       SerialAggregator.pop + optimize fused: the round's last drain and the
  *       server step in one pass              aggregators.py:104-122 + fedavg.py:193-208
  *
@@ -258,6 +258,19 @@ typedef struct fedagg_step_args {
 int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
                                    int64_t B, int64_t P, const float* acc_in, float W32,
                                    int flags, const fedagg_step_args* step, void* stream);
+
+/*
+ * The same fused last drain + server step over client rows that stay where
+ * the caller's tensors live (rows[k]: a device array of B device pointers,
+ * each to P contiguous, 16-byte aligned fp32), i.e. fedagg_reduce_rows_f32
+ * followed by fedagg_server_step_f32 in one pass.  This is the zero-copy
+ * round of HBM-resident client vectors (GPU-local training): no pack, no
+ * slab; SerialAggregator.add (aggregators.py:23-40) only records the row.
+ * Flags as for fedagg_reduce_step_blocked_f32 (FEDAGG_NT honoured).
+ */
+int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_t B,
+                                int64_t P, const float* acc_in, float W32, int flags,
+                                const fedagg_step_args* step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,7 @@ def test_header_declares_the_abi():
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
-        "fedagg_reduce_step_blocked_f32",
+        "fedagg_reduce_step_blocked_f32", "fedagg_reduce_step_rows_f32",
     ])
 
 
@@ -112,6 +112,13 @@ def test_argument_validation_without_device(lib):
     assert rs(16, 1 << 18, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(ok), null) == E  # 4 GiB
     misaligned = _native.StepArgs(0, 0.0, 20, None, None, None, 0, None, None, sgd)
     assert rs(16, 4, 4096, 16, 1, 4, null, 1.0, 3, ctypes.byref(misaligned), null) == E
+    rr = lib.fedagg_reduce_step_rows_f32
+    assert rr(16, 16, 1, 4, null, 1.0, 3, None, null) == E  # no step
+    assert rr(null, 16, 1, 4, null, 1.0, 3, ctypes.byref(ok), null) == E  # no row table
+    assert rr(16, 16, 1, 4, null, 1.0, 2, ctypes.byref(ok), null) == E  # no INIT, no acc
+    assert rr(16, 16, 1, 4, null, 1.0, 3 | 0x8, ctypes.byref(ok), null) == E  # SCALAR
+    assert rr(16, 16, 1, 4, null, 1.0, 3, ctypes.byref(misaligned), null) == E
+    assert rr(16, 16, 1, 4, null, 1.0, 3, ctypes.byref(ada_no_aux), null) == E
     assert lib.fedagg_server_step_f32(0, 16, 0.0, 16, null, null, null, 0, null, None, 4,
                                       null) == E  # no sgd params
     # P == 0 is a no-op success

@@ -1,0 +1,142 @@
+"""Zero-copy rounds of HBM-resident client vectors (SerialAggregator(borrow=True),
+fedagg_reduce_rows_f32 / fedagg_reduce_step_rows_f32): the client tensors are
+reduced where they live, in arrival order, bit for bit equal to the oracle and
+to the snapshotting path — across Bmax drains, interleaved with host adds,
+with get() in the middle, and fused with every server step."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import bits
+from oracle import ref
+from oracle import vectors as V
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available()
+    return torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("P", [1, 3, 4, 1023, 65_537, 1_085_668])
+@pytest.mark.parametrize("max_rows", [1, 3, 4096])
+def test_borrowed_rows_bitwise(P, max_rows, dev):
+    from fedsim_amd.utils import SerialAggregator
+
+    K = 23
+    X = V.client_rows("normal", K, P, 7)
+    w = V.client_weights("fedavg", K, 7)
+    agg = SerialAggregator(max_rows=max_rows, borrow=True)
+    rows = [torch.from_numpy(X[k].copy()).to(dev) for k in range(K)]
+    for k in range(K):
+        agg.add("p", rows[k], w[k])
+        if k == 11:
+            mid = agg.get("p")
+            np.testing.assert_array_equal(
+                bits(mid.cpu().numpy()), bits(ref.reduce(X[:12], w[:12], W=sum(w[:12]))))
+    assert len(agg._members["p"].borrowed) <= max(1, max_rows)
+    out = agg.pop("p")
+    assert out.device == dev
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref.reduce(X, w, W=sum(w))))
+
+
+def test_borrow_interleaved_with_host_and_unaligned_sources(dev):
+    """Host adds (snapshotted into the slab) and misaligned device views
+    (snapshotted too) between borrowed rows: arrival order is kept."""
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 17, 10_007
+    X = V.client_rows("realistic", K, P, 9)
+    w = V.client_weights("fednova", K, 9)
+    agg = SerialAggregator(borrow=True)
+    big = torch.empty(P + 1, device=dev)
+    for k in range(K):
+        if k % 4 == 1:
+            src = torch.from_numpy(X[k].copy())                 # host: slab path
+        elif k % 4 == 3:
+            big[1:].copy_(torch.from_numpy(X[k]))              # 4-B offset view: slab path
+            src = big[1:]
+        else:
+            src = torch.from_numpy(X[k].copy()).to(dev)        # borrowed
+        agg.add("p", src, w[k])
+        if k % 4 == 3:
+            big.fill_(float("nan"))  # the misaligned view was snapshotted at add
+    out = agg.pop("p")
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref.reduce(X, w, W=sum(w))))
+
+
+def test_borrowed_tensor_mutated_in_place_raises(dev):
+    from fedsim_amd.utils import SerialAggregator
+
+    agg = SerialAggregator(borrow=True)
+    t = torch.ones(4096, device=dev)
+    agg.add("p", t, 1)
+    t.mul_(2)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.pop("p")
+    # the snapshotting aggregator keeps the reference semantics instead
+    agg2 = SerialAggregator(borrow=False)
+    t = torch.ones(4096, device=dev)
+    agg2.add("p", t, 1)
+    t.mul_(2)
+    assert torch.equal(agg2.pop("p"), torch.ones(4096, device=dev))
+
+
+def test_borrowed_rows_on_another_stream(dev):
+    """Client tensors produced on a side stream: reading them on the compute
+    stream after the producer's work is ordered by the caller, and their
+    memory is not reused before the reduction ran (record_stream)."""
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 6, 300_001
+    X = V.client_rows("normal", K, P, 2)
+    w = [1] * K
+    side = torch.cuda.Stream(dev)
+    agg = SerialAggregator(borrow=True)
+    for k in range(K):
+        with torch.cuda.stream(side):
+            t = torch.from_numpy(X[k].copy()).to(dev, non_blocking=False)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        agg.add("p", t, w[k])
+        del t
+    out = agg.pop("p")
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref.reduce(X, w, W=K)))
+
+
+@pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_borrowed_pop_step_matches_two_step(algo, momentum, dev):
+    """pop_step over borrowed rows (one fedagg_reduce_step_rows_f32 launch)
+    == pop + fedagg_server_step_f32, bitwise, for every algorithm epilogue."""
+    from fedsim_amd import ops
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 9, 70_001
+    X = V.client_rows("realistic", K, P, 4)
+    w = V.client_weights("fedavg", K, 4)
+    cloud0 = torch.from_numpy(V.cloud_vector(P, 5)).to(dev)
+    aux0 = torch.from_numpy(V.cloud_vector(P, 6)).to(dev)
+    outs = []
+    for fused in (True, False):
+        agg = SerialAggregator(borrow=True)
+        for k in range(K):
+            agg.add("p", torch.from_numpy(X[k].copy()).to(dev), w[k])
+        cloud, aux = cloud0.clone(), aux0.clone()
+        buf = torch.empty_like(cloud) if momentum else None
+        grad = torch.empty_like(cloud)
+        step = ops.ServerStep(algo, cloud, lr=0.3, momentum=momentum, coef=0.6,
+                              aux=None if algo == "fedavg" else aux, momentum_buf=buf,
+                              momentum_init=True, grad_out=grad)
+        if fused:
+            agg.pop_step("p", step)
+        else:
+            step.apply(agg.pop("p").reshape(-1))
+        outs.append([t.cpu().numpy() for t in (cloud, aux, grad)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(bits(a), bits(b))
+    avg = ref.reduce(X, w, W=sum(w))
+    if algo == "fedavg" and not momentum:
+        np.testing.assert_array_equal(bits(outs[0][0]),
+                                      bits(ref.fedavg_sgd(avg, cloud0.cpu().numpy(), 0.3)))

@@ -4,8 +4,10 @@ reference's CPU-side local trainers), are snapshotted / DMA'd into the
 column-blocked HBM ring, reduced on the GPU, and the average comes back to the
 host (D2H included) — ``add`` x K + ``pop``, end to end, wall clock.
 
-Also times the D2D variant (vectors already in HBM, e.g. GPU local training)
-and reports the PCIe H2D copy ceiling measured on the same box.
+Also times the HBM-resident variants (vectors already in HBM, e.g. GPU local
+training): snapshotted into the slab by a D2D pack (device_d2d), or reduced in
+place through the row-pointer kernel (device_borrow, SerialAggregator(borrow=
+True)), and reports the PCIe H2D copy ceiling measured on the same box.
 
 python tools/bench_ingest.py [--K 200] [--P 25000000] [--pool 8] [--pinned]
 """
@@ -59,11 +61,12 @@ def main():
     host = [torch.randn(P) for _ in range(a.pool)]
     res = dict(K=K, P=P, pool=a.pool, threads=torch.get_num_threads(),
                h2d_ceiling_GBps=h2d_ceiling(P, dev))
-    for name, pool in (("host_pageable", host),
-                       ("host_pinned", [t.pin_memory() for t in host]),
-                       ("device_d2d", [t.to(dev) for t in host])):
-        run_round(pool, weights, min(K, 2 * a.pool))  # warm-up (allocations, pinned cache)
-        ts = [run_round(pool, weights, K) for _ in range(a.reps)]
+    for name, pool, kw in (("host_pageable", host, {}),
+                           ("host_pinned", [t.pin_memory() for t in host], {}),
+                           ("device_d2d", [t.to(dev) for t in host], {}),
+                           ("device_borrow", [t.to(dev) for t in host], dict(borrow=True))):
+        run_round(pool, weights, min(K, 2 * a.pool), **kw)  # warm-up (allocations, pinned cache)
+        ts = [run_round(pool, weights, K, **kw) for _ in range(a.reps)]
         t = min(ts)
         res[name] = dict(seconds=t, GBps=4.0 * K * P / t / 1e9)
         del pool
