@@ -1,0 +1,96 @@
+"""End-to-end server round through the plugin surface, as a FedSim run drives
+it: ``FedAvg.receive_from_client`` x K (serial_aggregation -> SerialAggregator
+.add, plus the per-split scalar metrics) and ``FedAvg.optimize`` (pop + server
+SGD step, fused into the round's last reduction).  Wall clock per round, split
+into the host-side receive loop and the rest, for client vectors that are
+
+  device_borrow   HBM-resident tensors handed over (the round driver's default)
+  device_snap     HBM-resident tensors snapshotted at add (borrow=False)
+  host_pinned     pinned host tensors (CPU-side local trainers)
+
+and, for reference, the device-resident kernel time of the same reduce + step
+(tools/bench_configs.py).
+
+python tools/bench_plugin_round.py [--only cfg2_K1000] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedsim_amd.distributed.centralized.training import FedAvg  # noqa: E402
+from fedsim_amd.utils import SerialAggregator, Storage  # noqa: E402
+
+CONFIGS = {
+    "cfg1": (5, 199_210),
+    "cfg2_K10": (10, 1_085_668),
+    "cfg2_K1000": (1000, 1_085_668),
+}
+
+
+def messages(K, P, where, dev, seed=11):
+    weights = [int(v) for v in np.random.default_rng(seed).integers(50, 601, size=K)]
+    g = torch.Generator(device=dev).manual_seed(seed)
+    msgs = []
+    for k in range(K):
+        t = torch.empty(P, device=dev).normal_(0.0, 0.05, generator=g)
+        if where == "host_pinned":
+            t = t.cpu().pin_memory()
+        msgs.append(dict(local_params=t, num_steps=1, diverged=False,
+                         num_samples={"train": weights[k]},
+                         metrics={"train": {"cross_entropy_score": 1.0 + 1e-3 * k}}))
+    return msgs
+
+
+def one_round(msgs, cloud, borrow):
+    st = Storage()
+    st.write("cloud_params", cloud)
+    st.write("optimizer", torch.optim.SGD(params=[cloud], lr=1.0))
+    st.write("lr_scheduler", None)
+    agg = SerialAggregator(expected_rows=len(msgs), borrow=borrow)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k, msg in enumerate(msgs):
+        FedAvg.receive_from_client(st, k, dict(msg), "train", agg, None)
+    t1 = time.perf_counter()
+    FedAvg.optimize(st, agg, None)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    return t1 - t0, t2 - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    names = [n for n in CONFIGS if not a.only or n in a.only.split(",")]
+    out = {}
+    for name in names:
+        K, P = CONFIGS[name]
+        res = dict(K=K, P=P)
+        for where, borrow in (("device_borrow", True), ("device_snap", False),
+                              ("host_pinned", False)):
+            msgs = messages(K, P, where, dev)
+            cloud = torch.zeros(P, device=dev, requires_grad=True)
+            one_round(msgs, cloud, borrow)  # warm-up
+            runs = [one_round(msgs, cloud, borrow) for _ in range(a.reps)]
+            recv, total = min(r[0] for r in runs), min(r[1] for r in runs)
+            res[where] = dict(round_ms=total * 1e3, receive_loop_ms=recv * 1e3,
+                              per_client_us=recv / K * 1e6,
+                              client_GBps=4.0 * K * P / total / 1e9)
+            del msgs, cloud
+            torch.cuda.empty_cache()
+        out[name] = res
+        print(json.dumps({name: res}), flush=True)
+    print(json.dumps({"all": out}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
