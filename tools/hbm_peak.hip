@@ -8,7 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
+#include <string>
 
 #define CHECK(x)                                                                   \
   do {                                                                             \
@@ -39,6 +41,106 @@ __global__ __launch_bounds__(256) void read_stream(const f32x4* __restrict__ x, 
   if (acc.x + acc.y + acc.z + acc.w == 12345.678f) sink[0] = 1.f;  // keep live
 }
 
+// (c) chunked read: workgroup b streams its own contiguous chunk of `chunk`
+// f32x4 slots (the access shape of the blocked reduce kernel: one region per
+// workgroup, rows of BS*VPT slots inside it), VPT slots per lane, U rows of
+// loads in flight.
+template <int BS, int VPT, int U>
+__global__ __launch_bounds__(BS) void read_chunk(const f32x4* __restrict__ x, size_t chunk,
+                                                 float* __restrict__ sink) {
+  const f32x4* base = x + static_cast<size_t>(blockIdx.x) * chunk;
+  constexpr int ROW = BS * VPT;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const size_t rows = chunk / ROW;
+  size_t r = 0;
+  for (; r + U <= rows; r += U) {
+    f32x4 v[U][VPT];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j)
+        v[u][j] = __builtin_nontemporal_load(base + (r + u) * ROW + j * BS + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) acc += v[u][j];
+  }
+  for (; r < rows; ++r)
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) acc += base[r * ROW + j * BS + threadIdx.x];
+  if (acc.x + acc.y + acc.z + acc.w == 12345.678f) sink[0] = 1.f;
+}
+
+// (d) the reduce kernel's access shape under two slab layouts, K rows x nblk
+// column blocks of 4096 floats (1024 f32x4 = 256 lanes x 4 slots):
+//   KB == K : column-blocked [nblk][K][C]       (one 16 MB region per workgroup)
+//   KB <  K : row-grouped    [K/KB][nblk][KB][C] (workgroup b reads group g's
+//             KB rows of block b, KB*16 KB contiguous, then group g+1; the
+//             workgroups running together stay inside one nblk*KB*16 KB window)
+// Weighted running sums in registers, U rows of loads in flight.
+template <int KB, int U>
+__global__ __launch_bounds__(256) void reduce_shape(const f32x4* __restrict__ x, int K,
+                                                   int nblk, const float* __restrict__ w,
+                                                   float* __restrict__ sink) {
+  constexpr int ROW = 1024;
+  const int b = blockIdx.x;
+  f32x4 a[4] = {};
+  for (int g = 0; g < K / KB; ++g) {
+    const f32x4* base = x + (static_cast<size_t>(g) * nblk + b) * KB * ROW;
+    for (int kk = 0; kk < KB; kk += U) {
+      f32x4 v[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[u][j] = __builtin_nontemporal_load(base + (kk + u) * ROW + j * 256 + threadIdx.x);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float wk = w[g * KB + kk + u];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = a[j] + v[u][j] * wk;
+      }
+    }
+  }
+  const f32x4 t = a[0] + a[1] + a[2] + a[3];
+  if (t.x + t.y + t.z + t.w == 12345.678f) sink[0] = 1.f;
+}
+
+// (e) the blocked reduce shape with a runtime region pitch (in f32x4) and an
+// optional XCD-aware workgroup -> region remap: region r = remap(blockIdx.x).
+template <int U>
+__global__ __launch_bounds__(256) void reduce_pitch(const f32x4* __restrict__ x, int K,
+                                                   size_t pitch, int nblk, int remap,
+                                                   const float* __restrict__ w,
+                                                   float* __restrict__ sink) {
+  constexpr int ROW = 1024;
+  int b = blockIdx.x;
+  if (remap) {  // dispatch is round-robin over 8 XCDs: give each XCD a contiguous range
+    const int per = (nblk + 7) / 8;
+    const int xcd = b % 8, i = b / 8;
+    b = xcd * per + i;
+    if (b >= nblk) return;
+  }
+  const f32x4* base = x + static_cast<size_t>(b) * pitch;
+  f32x4 a[4] = {};
+  for (int k = 0; k + U <= K; k += U) {
+    f32x4 v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[u][j] = __builtin_nontemporal_load(base + (k + u) * ROW + j * 256 + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wk = w[k + u];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = a[j] + v[u][j] * wk;
+    }
+  }
+  const f32x4 t = a[0] + a[1] + a[2] + a[3];
+  if (t.x + t.y + t.z + t.w == 12345.678f) sink[0] = 1.f;
+}
+
 __global__ __launch_bounds__(256) void copy_stream(const f32x4* __restrict__ x,
                                                    f32x4* __restrict__ y, size_t n) {
   const size_t stride = static_cast<size_t>(gridDim.x) * 256;
@@ -62,7 +164,132 @@ static float time_ms(F f, int iters) {
   return ms / iters;
 }
 
+// Second sweep (argv[2] == "sweep2"): wider grids / deeper unroll for the
+// grid-stride stream, and the chunked (per-workgroup region) shape at several
+// region sizes.
+static void sweep2(const f32x4* x, size_t n, size_t bytes, float* sink) {
+  std::printf("{\"read_stream\": [");
+  bool first = true;
+  const int grids[] = {16384, 32768, 65536};
+  for (int g : grids) {
+#define RUN2(U)                                                                        \
+  {                                                                                    \
+    float ms = time_ms([&] { read_stream<U, true><<<g, 256>>>(x, n, sink); }, 5);     \
+    std::printf("%s{\"grid\": %d, \"unroll\": %d, \"GBps\": %.1f}", first ? "" : ", ", \
+                g, U, bytes / ms / 1e6);                                               \
+    first = false;                                                                     \
+  }
+    RUN2(8) RUN2(16)
+  }
+  std::printf("], \"read_chunk\": [");
+  first = true;
+  const size_t chunks_kib[] = {64, 256, 1024, 4096, 16384};
+  for (size_t ck : chunks_kib) {
+    const size_t chunk = ck * 1024 / 16;
+    const size_t nblk = n / chunk;
+    const double b = static_cast<double>(nblk) * chunk * 16;
+#define RUNC(BS, VPT, U)                                                                 \
+  {                                                                                      \
+    float ms = time_ms([&] { read_chunk<BS, VPT, U><<<nblk, BS>>>(x, chunk, sink); }, 5); \
+    std::printf("%s{\"chunk_KiB\": %zu, \"bs\": %d, \"vpt\": %d, \"unroll\": %d, "     \
+                "\"GBps\": %.1f}", first ? "" : ", ", ck, BS, VPT, U, b / ms / 1e6);       \
+    first = false;                                                                       \
+  }
+    RUNC(256, 4, 4) RUNC(256, 4, 8) RUNC(256, 2, 8) RUNC(512, 2, 4) RUNC(256, 1, 16)
+  }
+  std::printf("]}\n");
+}
+
+// Third sweep (argv[1] == "layout"): reduce_shape over K=1024 rows x 6104
+// column blocks (25 M columns, 102 GB), blocked vs row-grouped layouts.
+static int layout_sweep() {
+  const int K = 1024, nblk = 6104;
+  const size_t bytes = static_cast<size_t>(K) * nblk * 4096 * 4;
+  f32x4* x;
+  float *w, *sink;
+  CHECK(hipMalloc(&x, bytes));
+  CHECK(hipMemset(x, 0x3c, bytes));
+  CHECK(hipMalloc(&w, K * 4));
+  CHECK(hipMemset(w, 0x3c, K * 4));
+  CHECK(hipMalloc(&sink, 4));
+  std::printf("{\"K\": %d, \"nblk\": %d, \"bytes\": %zu, \"reduce_shape\": [", K, nblk, bytes);
+  bool first = true;
+#define RUNL(KB, U)                                                                      \
+  {                                                                                      \
+    float ms = time_ms([&] { reduce_shape<KB, U><<<nblk, 256>>>(x, K, nblk, w, sink); }, 3); \
+    std::printf("%s{\"KB\": %d, \"unroll\": %d, \"ms\": %.3f, \"GBps\": %.1f}",          \
+                first ? "" : ", ", KB, U, ms, bytes / ms / 1e6);                         \
+    first = false;                                                                       \
+  }
+  RUNL(1024, 4) RUNL(4, 4) RUNL(8, 4) RUNL(16, 4) RUNL(32, 4) RUNL(64, 4) RUNL(128, 4)
+  RUNL(256, 4) RUNL(16, 8) RUNL(32, 8) RUNL(1024, 4)
+  std::printf("]}\n");
+  CHECK(hipFree(x));
+  CHECK(hipFree(w));
+  CHECK(hipFree(sink));
+  return 0;
+}
+
+// Random-bit fill (data-dependent power: a stream of constant words toggles
+// far fewer bits than real client updates do).
+__global__ void fill_random(uint32_t* p, size_t n) {
+  for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * 256) {
+    uint64_t z = i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    // a finite float in [0.5, 1) with random mantissa and sign
+    p[i] = 0x3f000000u | (static_cast<uint32_t>(z) & 0x807fffffu);
+  }
+}
+
+// Fourth sweep (argv[1] == "pitch"): K=1000 rows x 6104 blocks (the headline
+// slab), region pitch = K*16 KiB + skew, with / without the XCD remap.
+static int pitch_sweep() {
+  const int K = 1000, nblk = 6104;
+  const size_t region = static_cast<size_t>(K) * 1024;  // f32x4
+  const size_t skews[] = {0, 16, 64, 256, 1024, 4096};    // f32x4 (x16 B)
+  const size_t maxb = (region + 4096) * nblk * 16;
+  f32x4* x;
+  float *w, *sink;
+  CHECK(hipMalloc(&x, maxb));
+  CHECK(hipMalloc(&w, K * 4));
+  CHECK(hipMemset(w, 0x3c, K * 4));
+  CHECK(hipMalloc(&sink, 4));
+  const double bytes = static_cast<double>(region) * nblk * 16;
+  std::printf("{\"K\": %d, \"nblk\": %d, \"reduce_pitch\": [", K, nblk);
+  bool first = true;
+  for (int rep = 0; rep < 2; ++rep)
+    for (int data = 0; data < 2; ++data) {
+     if (data == 0)
+       CHECK(hipMemset(x, 0x3c, maxb));
+     else
+       fill_random<<<8192, 256>>>(reinterpret_cast<uint32_t*>(x), maxb / 4);
+     CHECK(hipDeviceSynchronize());
+     for (size_t sk : skews)
+      for (int remap = 0; remap < 2; ++remap) {
+        if (sk > 256 || remap) continue;
+        const size_t pitch = region + sk;
+        const int grid = remap ? (nblk + 7) / 8 * 8 : nblk;
+        float ms = time_ms(
+            [&] { reduce_pitch<4><<<grid, 256>>>(x, K, pitch, nblk, remap, w, sink); }, 3);
+        std::printf("%s{\"data\": \"%s\", \"skew_B\": %zu, \"remap\": %d, \"ms\": %.3f, "
+                    "\"GBps\": %.1f}", first ? "" : ", ", data ? "random" : "const", sk * 16,
+                    remap, ms, bytes / ms / 1e6);
+        first = false;
+      }
+    }
+  std::printf("]}\n");
+  CHECK(hipFree(x));
+  CHECK(hipFree(w));
+  CHECK(hipFree(sink));
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "layout") return layout_sweep();
+  if (argc > 1 && std::string(argv[1]) == "pitch") return pitch_sweep();
   const double gib = argc > 1 ? std::atof(argv[1]) : 32.0;
   const size_t bytes = static_cast<size_t>(gib * (1ull << 30)) / 16 * 16;
   const size_t n = bytes / 16;
@@ -72,6 +299,12 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&x, bytes));
   CHECK(hipMemset(x, 0x3c, bytes));
   CHECK(hipMalloc(&sink, 4));
+  if (argc > 2 && std::string(argv[2]) == "sweep2") {
+    sweep2(x, n, bytes, sink);
+    CHECK(hipFree(x));
+    CHECK(hipFree(sink));
+    return 0;
+  }
   const int grids[] = {2048, 4096, 8192, 16384};
   std::printf("{\"read_stream\": [");
   bool first = true;
