@@ -140,3 +140,47 @@ def test_borrowed_pop_step_matches_two_step(algo, momentum, dev):
     if algo == "fedavg" and not momentum:
         np.testing.assert_array_equal(bits(outs[0][0]),
                                       bits(ref.fedavg_sgd(avg, cloud0.cpu().numpy(), 0.3)))
+
+
+def test_borrowed_full_size_round(dev):
+    """Headline size through the borrowing aggregator: 1000 separate HBM
+    client tensors of 25 M floats (100 GB).  The default HBM budget makes the
+    aggregator drain once in the middle (accumulator chaining) and fuse the
+    FedAvg step into the last drain; the result equals one pass of the
+    row-pointer kernel bitwise, and the oracle on 4096 sampled columns."""
+    from fedsim_amd import ops
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 1000, 25_000_000
+    torch.cuda.empty_cache()  # earlier tests' cached blocks count as used
+    free, _ = torch.cuda.mem_get_info(dev)
+    if free < 130e9:
+        pytest.skip("needs >130 GB of free HBM")
+    g = torch.Generator(device=dev).manual_seed(8)
+    rows = [torch.empty(P, device=dev).normal_(0.0, 0.05, generator=g) for _ in range(K)]
+    w = [int(v) for v in np.random.default_rng(11).integers(50, 601, size=K)]
+    W = sum(w)
+    agg = SerialAggregator(borrow=True)
+    entry = None
+    drains = 0
+    for k in range(K):
+        agg.add("p", rows[k], w[k])
+        entry = agg._members["p"]
+        drains += entry.acc is not None and len(entry.borrowed) == 1 and k > 0
+    assert entry.Bmax < K and drains >= 1  # at least one chained drain happened
+    cloud = torch.zeros(P, device=dev)
+    step = ops.ServerStep("fedavg", cloud, lr=1.0)
+    agg.pop_step("p", step)
+    # one pass over the same rows, then the same step on the stored average
+    avg = torch.empty(P, device=dev)
+    w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
+    ops.reduce_rows(rows, w32, avg, W=W, flags=ops.FEDAGG_NT)
+    cloud2 = torch.zeros(P, device=dev)
+    ops.ServerStep("fedavg", cloud2, lr=1.0).apply(avg)
+    assert torch.equal(cloud.view(torch.int32), cloud2.view(torch.int32))
+    cols = torch.from_numpy(np.random.default_rng(3).choice(P, size=4096, replace=False)).to(dev)
+    sub = torch.stack([r.index_select(0, cols) for r in rows]).cpu().numpy()
+    exp_avg = ref.reduce(sub, w, W=W)
+    np.testing.assert_array_equal(bits(avg.index_select(0, cols).cpu().numpy()), bits(exp_avg))
+    exp_cloud = ref.fedavg_sgd(exp_avg, np.zeros(4096, np.float32), 1.0)
+    np.testing.assert_array_equal(bits(cloud.index_select(0, cols).cpu().numpy()), bits(exp_cloud))
