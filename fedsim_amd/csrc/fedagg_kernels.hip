@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/fedagg.h"
 
 // The reference rounds every product and every sum separately; forbid the
@@ -50,6 +52,8 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 constexpr int kDefaultUnroll = 4;
 constexpr int kDefaultVptSel = 2;  // 2 float4 slots per lane
 constexpr int kDefaultBsSel = 1;   // blocked layout: 256-lane workgroups
+constexpr int kRowsUnroll = 4;     // row-pointer fused step (fedagg_reduce_step_rows_f32)
+constexpr int kRowsVpt = 2;
 constexpr int kWeightTile = 2048;  // FEDAGG_LDSW ablation: weights per LDS tile
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
@@ -122,6 +126,28 @@ struct RowsTable {
   }
   template <bool NT>
   __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const;
+};
+
+// Row-pointer table loaded with buffer instructions: row k's base pointer is a
+// wave-uniform scalar load from the table, turned into a buffer descriptor in
+// SGPRs, and the lane's column stays a 32-bit VGPR voffset, so the unrolled
+// loop holds no 64-bit VGPR address per in-flight load:
+//   s_load_dwordx2 s[base], s[tab], k*8 ; buffer_load_dwordx4 v, v_off, s[rsrc], 0 offen
+struct RowsTableBuf {
+  const float* const* rows;
+  uint32_t row_bytes;  // 4*P, clamped to the 32-bit field (table_row_bytes)
+  __device__ __forceinline__ const char* row(int64_t k) const {
+    return reinterpret_cast<const char*>(rows[k]);
+  }
+  template <bool NT>
+  __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const {
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(rows[k]), static_cast<short>(0), static_cast<int>(row_bytes),
+        0x00020000);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(goff), 0,
+                                                          NT ? 2 : 0);
+    return __builtin_bit_cast(f32x4, v);
+  }
 };
 
 template <bool NT>
@@ -680,6 +706,13 @@ hipError_t dispatch_blocked(const Rows& rows, int64_t C, int bs_sel, const float
   return hipErrorInvalidValue;
 }
 
+// num_records of a row's buffer descriptor: 4*P bytes, clamped to the 32-bit
+// field (P == 2^30 is the largest accepted size).
+uint32_t table_row_bytes(int64_t P) {
+  const int64_t b = P * 4;
+  return b >= (int64_t(1) << 32) ? 0xFFFFFFFFu : static_cast<uint32_t>(b);
+}
+
 int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
                       const float* out, int flags) {
   if (B < 0 || P < 0) return FEDAGG_EINVAL;
@@ -774,9 +807,13 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
   // sync: the caller passes FEDAGG_SCALAR unless every rows[k] is 16-B aligned.
   const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(out) &&
                       ((flags & FEDAGG_INIT) || aligned16(acc_in));
-  RowsTable tab{rows};
-  return static_cast<int>(dispatch_reduce(tab, vec_ok, w, B, P, acc_in, out, W32, flags,
-                                          static_cast<hipStream_t>(stream)));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // buffer-descriptor loads unless asked for flat 64-bit addressing
+  if (flags & FEDAGG_FLAT)
+    return static_cast<int>(
+        dispatch_reduce(RowsTable{rows}, vec_ok, w, B, P, acc_in, out, W32, flags, s));
+  return static_cast<int>(dispatch_reduce(RowsTableBuf{rows, table_row_bytes(P)}, vec_ok, w, B, P,
+                                          acc_in, out, W32, flags, s));
 }
 
 int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
@@ -950,20 +987,25 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   if (rc != 0) return rc;
   rc = check_reduce_args(w, B, P, acc_in, step->cloud, flags);
   if (rc != 0 || P == 0) return rc;
-  if (flags & (FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
+  if (flags & (FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
   if (B > 0 && !rows) return FEDAGG_EINVAL;
   if (!step_aligned(sp) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in))) return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const RowsTable tab{rows};
-  // the rows path's default configuration (256 lanes, 2 float4 slots per
-  // lane, U = 4); the rows are the caller's separate allocations
+  // the rows path's default configuration (256 lanes, kRowsVpt float4 slots
+  // per lane, U = kRowsUnroll); the rows are the caller's separate
+  // allocations, read through buffer descriptors unless FEDAGG_FLAT
   const bool nt = (flags & FEDAGG_NT) != 0;
-  hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
-    return nt ? launch_vec<kBlock, kDefaultUnroll, 2, true, RowsTable, false>(
-                    tab, w, B, P, acc_in, epi, W32, flags, s)
-              : launch_vec<kBlock, kDefaultUnroll, 2, false, RowsTable, false>(
-                    tab, w, B, P, acc_in, epi, W32, flags, s);
-  });
+  auto go = [&](const auto& tab) {
+    using T = std::decay_t<decltype(tab)>;
+    return with_step(step->algo, mom, sp, [&](auto epi) {
+      return nt ? launch_vec<kBlock, kRowsUnroll, kRowsVpt, true, T, false>(tab, w, B, P, acc_in,
+                                                                          epi, W32, flags, s)
+                : launch_vec<kBlock, kRowsUnroll, kRowsVpt, false, T, false>(
+                      tab, w, B, P, acc_in, epi, W32, flags, s);
+    });
+  };
+  hipError_t e = (flags & FEDAGG_FLAT) ? go(RowsTable{rows})
+                                       : go(RowsTableBuf{rows, table_row_bytes(P)});
   if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
   return static_cast<int>(e);
 }

@@ -1,8 +1,10 @@
-"""Centralized FL algorithms on the MI355X aggregation path.
+"""Algorithm plugins whose server side runs on the MI355X aggregation path.
 
-Attribute lookup mirrors ``fedsim.distributed.centralized.training``
-(training/__init__.py:8-23) so that a ``--algorithm FedAvg`` style resolution
-(fedsim_cli/utils.py:186-192) finds the same names here.
+The CLI of the reference resolves ``--algorithm <Name>`` by attribute lookup
+on its training package (fedsim_cli/utils.py:186-192 over
+fedsim/distributed/centralized/training/__init__.py), so every class is
+exported here under the reference's name.  ``ALGORITHMS`` / ``get_algorithm``
+offer the same resolution without the CLI.
 """
 from .adabest import AdaBest
 from .fedavg import FedAvg
@@ -12,4 +14,15 @@ from .fednova import FedNova
 from .fedprox import FedProx
 from .utils import serial_aggregation
 
-__all__ = ["FedAvg", "AdaBest", "FedDyn", "FedNova", "FedProx", "FedDF", "serial_aggregation"]
+ALGORITHMS = {cls.__name__: cls for cls in (FedAvg, AdaBest, FedDyn, FedNova, FedProx, FedDF)}
+
+
+def get_algorithm(name: str):
+    """The plugin class called ``name`` (as ``--algorithm name`` would find it)."""
+    try:
+        return ALGORITHMS[name]
+    except KeyError:
+        raise ValueError(f"unknown algorithm {name!r}; have {sorted(ALGORITHMS)}") from None
+
+
+__all__ = [*ALGORITHMS, "serial_aggregation", "ALGORITHMS", "get_algorithm"]

@@ -23,6 +23,8 @@ from typing import Optional
 import torch
 
 from .... import ops
+from ....local import local_inference
+from ....utils import initialize_module, vectorize_module
 from ....utils.aggregators import SerialAggregator as _DeviceSerialAggregator
 
 
@@ -165,3 +167,58 @@ def fused_server_step(algo: str, cloud: torch.Tensor, avg, optimizer,
     x_out = None if x is None else x.view_as(aux).to(aux.device)
     ap_out = None if ap is None else ap.view_as(cloud).to(cloud.device)
     return x_out, ap_out
+
+
+# ---------------------------------------------------------------------------
+# Server-side state shared by the FedAvg family (fedavg.py:70-85, 210-256)
+# ---------------------------------------------------------------------------
+def init_cloud(server_storage):
+    """Build the cloud model on the server device and its flat parameter
+    vector (the tensor the fused server step updates in place), plus the
+    server optimizer / LR scheduler over ``[cloud_params]``."""
+    model = server_storage.read("model_def")().to(server_storage.read("device"))
+    cloud = vectorize_module(model, clone=True, detach=True)
+    cloud.requires_grad = True
+    opt = server_storage.read("optimizer_def")(params=[cloud])
+    sched_def = server_storage.read("lr_scheduler_def")
+    for key, obj in (("model", model), ("cloud_params", cloud), ("optimizer", opt),
+                     ("lr_scheduler", None if sched_def is None else sched_def(optimizer=opt))):
+        server_storage.write(key, obj)
+    return cloud
+
+
+def init_drift_state(server_storage):
+    """``avg_params`` (last round's average) and the zero ``h`` vector that
+    AdaBest and FedDyn keep next to the cloud vector."""
+    cloud = server_storage.read("cloud_params")
+    server_storage.write("avg_params", cloud.clone().detach())
+    server_storage.write("h", torch.zeros_like(cloud))
+
+
+def cloud_model_message(server_storage):
+    """The cloud vector unflattened into the server's model (views of one
+    device-resident vector, see utils/convert_parameters.py)."""
+    model = server_storage.read("model")
+    initialize_module(model, server_storage.read("cloud_params"), clone=True, detach=True)
+    return dict(model=model)
+
+
+NORM_REPORT_FREQ = 50
+
+
+def deployment_report(server_storage, dataloaders, rounds, scores, device, optimize_reports,
+                      deployment_points=None):
+    """Scores of every deployment point on every scored server split, plus the
+    point's parameter norm every NORM_REPORT_FREQ rounds."""
+    model = server_storage.read("model")
+    out, norms = dict(), dict()
+    for point_name, point in (deployment_points or dict()).items():
+        initialize_module(model, point, clone=True, detach=True)
+        for split_name, loader in dataloaders.items():
+            if split_name in scores:
+                local_inference(model, loader, scores=scores[split_name], device=device)
+                for score_name, score in scores[split_name].items():
+                    out[f"server.{point_name}.{split_name}.{score_name}"] = score.get_score()
+            if rounds % NORM_REPORT_FREQ == 0:
+                norms[f"server.{point_name}.param.norm"] = point.norm().item()
+    return {**out, **optimize_reports, **norms}

@@ -457,10 +457,13 @@ def reduce_rows_step(
     W: Optional[float] = None,
     nt: bool = True,
     table: Optional[torch.Tensor] = None,
+    flat: bool = False,
 ) -> torch.Tensor:
     """reduce_rows(rows, ..., out=avg) then step.apply(avg), fused into one
     pass over the caller's own client tensors (fedagg_reduce_step_rows_f32):
-    the zero-copy round of HBM-resident client vectors.  Returns step.cloud."""
+    the zero-copy round of HBM-resident client vectors.  Returns step.cloud.
+    ``flat`` selects 64-bit flat loads instead of per-row buffer descriptors
+    (ablation; same arithmetic)."""
     _require_hip_f32(w32, "w32")
     P, dev = step.P, step.cloud.device
     B = len(rows)
@@ -474,7 +477,7 @@ def reduce_rows_step(
         raise ValueError("w32 too short")
     if not step.aligned():
         raise ValueError("every server-step operand must be 16-B aligned")
-    f = FEDAGG_NT if nt else 0
+    f = (FEDAGG_NT if nt else 0) | (_native.FEDAGG_FLAT if flat else 0)
     if acc_in is None:
         f |= FEDAGG_INIT
     else:

@@ -1,4 +1,13 @@
-"""Host-side utilities of the accelerated server path."""
+"""Host-side objects around the HIP aggregation path.
+
+* ``SerialAggregator`` — the reference's duck type (add / get / pop /
+  get_sum / get_weight / pop_all / items / keys / in) backed by libfedagg:
+  tensor keys are reduced in HBM, scalar keys keep the reference's host
+  arithmetic.  ``DeviceAggregator`` is its tensor-only core.
+* ``AppendixAggregator`` — the keep-every-value aggregator FedDF uses.
+* ``Storage`` — server / client key-value memory with access protection.
+* parameter packing (``vectorize_module`` ...) — flat fp32 vectors and views.
+"""
 from .aggregators import AppendixAggregator, DeviceAggregator, SerialAggregator
 from .convert_parameters import (
     initialize_module,
@@ -10,13 +19,7 @@ from .dict_ops import apply_on_dict
 from .storage import Storage
 
 __all__ = [
-    "SerialAggregator",
-    "DeviceAggregator",
-    "AppendixAggregator",
-    "Storage",
-    "apply_on_dict",
-    "vectorize_module",
-    "initialize_module",
-    "vector_to_parameters_like",
+    "SerialAggregator", "DeviceAggregator", "AppendixAggregator", "Storage", "apply_on_dict",
+    "vectorize_module", "initialize_module", "vector_to_parameters_like",
     "vector_to_named_parameters_like",
 ]

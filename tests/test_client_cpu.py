@@ -1,9 +1,11 @@
 """Client side (the producer of the aggregated vectors), on CPU: one client's
 ``send_to_server`` — local SGD through local_train / default_step_closure and
-the CrossEntropyScore criterion, FedProx's proximal gradient term — reproduces
+the CrossEntropyScore criterion, FedProx's proximal gradient term, AdaBest's
+and FedDyn's drift terms and their client-side h over two calls — reproduces
 the reference's own output bit for bit on the goldens' CPU, within 1e-5
 normwise on another (tests/golden/rounds.json "clients",
-made by tools/gen_golden_rounds.py from fedprox.py:68-127 / fedavg.py:88-179)."""
+made by tools/gen_golden_rounds.py from fedprox.py:68-127 / fedavg.py:88-179 /
+adabest.py:97-148 / feddyn.py:104-155)."""
 import json
 import os
 from functools import partial
@@ -32,6 +34,7 @@ def arrays():
 def test_send_to_server_matches_reference(case, arrays):
     from fedsim_amd import scores
     from fedsim_amd.distributed.centralized import training
+    from fedsim_amd.utils import Storage
 
     cls = getattr(training, case["algorithm"])
     lopt = case["local_opt"]
@@ -44,12 +47,21 @@ def test_send_to_server_matches_reference(case, arrays):
               **case["alg_kwargs"])
     st = alg.get_server_storage()
     cid = case["client_id"]
-    ctx = cls.send_to_client(st, cid)
-    torch.manual_seed(1000 + cid)
-    msg = cls.send_to_server(cid, case["rounds"], None, dm.get_local_dataset(cid), "train", {},
-                             2, scores.CrossEntropyScore(), 32, 64,
-                             partial(torch.optim.SGD, **lopt), None, "cpu", ctx=ctx)
+    multi = isinstance(case["rounds"], list)  # successive calls on one client storage
+    cstore = Storage() if multi else None
+    for i, rounds in enumerate(case["rounds"] if multi else [case["rounds"]]):
+        ctx = cls.send_to_client(st, cid)
+        torch.manual_seed(1000 + cid + 17 * i)
+        msg = cls.send_to_server(cid, rounds, cstore, dm.get_local_dataset(cid), "train", {},
+                                 2, scores.CrossEntropyScore(), 32, 64,
+                                 partial(torch.optim.SGD, **lopt), None, "cpu", ctx=ctx)
     got, want = msg["local_params"].numpy(), arrays[f"{case['id']}/local_params"]
+    if multi:  # the client-side drift / dual vector h the calls left behind
+        h, h_want = cstore.read("h").numpy(), arrays[f"{case['id']}/h"]
+        if SAME_HOST:
+            np.testing.assert_array_equal(bits(h), bits(h_want))
+        else:
+            assert np.linalg.norm(h.astype(np.float64) - h_want) <= 1e-5 * np.linalg.norm(h_want)
     assert msg["num_steps"] == case["num_steps"]
     assert msg["diverged"] == case["diverged"]
     assert msg["num_samples"] == case["num_samples"]

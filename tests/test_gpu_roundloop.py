@@ -14,7 +14,8 @@ teacher / distillation forwards — are bitwise only on device="cpu" on a host
 whose CPU matches the one that made the goldens (oracle/synthetic_fl.py
 host_signature: MKL/oneDNN GEMMs round per ISA and vendor).  On the GPU
 (rocBLAS/MIOpen) or another CPU they are held to a normwise tolerance:
-||cloud - golden|| <= 1e-4 ||golden|| after 5 rounds, and the score report
+||cloud - golden|| <= 1e-4 ||golden|| after 5 rounds (FedDyn's h, a running
+sum of cloud - avg differences, against ||cloud||), and the score report
 within 1e-4 relative."""
 import json
 import os
@@ -86,7 +87,11 @@ def test_round_loop_matches_reference(run, device, arrays):
         if exact:
             np.testing.assert_array_equal(bits(got), bits(want))
         else:
-            err = np.linalg.norm(got.astype(np.float64) - want) / np.linalg.norm(want)
+            # h (FedDyn's dual vector) accumulates r * (cloud - avg), a
+            # difference of two cloud-sized vectors: its rounding noise scales
+            # with ||cloud||, not with its own (small) norm
+            ref_norm = np.linalg.norm(arrays[f"{run['id']}/cloud"] if name == "h" else want)
+            err = np.linalg.norm(got.astype(np.float64) - want) / ref_norm
             print(f"{run['id']} {run['algorithm']} {name}: normwise rel err {err:.3e}")
             assert err <= RTOL
     got_scores = {k: float(v) for k, v in scores.items()}

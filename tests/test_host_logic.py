@@ -271,3 +271,17 @@ def test_pack_unpack_layout_and_views():
     assert torch.equal(named["3.bias"], model[3].bias.detach())
     with pytest.raises(TypeError):
         vector_to_parameters_like([1.0], model.parameters())
+
+
+def test_algorithm_registry_resolves_reference_names():
+    """--algorithm <Name> resolution (fedsim_cli/utils.py:186-192): every
+    reference class name maps to the plugin exported under that name."""
+    from fedsim_amd.distributed import centralized
+    from fedsim_amd.distributed.centralized import training
+
+    for name in ("FedAvg", "AdaBest", "FedDyn", "FedNova", "FedProx", "FedDF"):
+        cls = training.get_algorithm(name)
+        assert cls is getattr(training, name) is getattr(centralized, name)
+        assert cls.__name__ == name
+    with pytest.raises(ValueError):
+        training.get_algorithm("FedSGD")

@@ -41,6 +41,8 @@ RUNS = [
     ("FedAvg", dict(), dict(lr=1.0), "local", 0),
     ("FedProx", dict(mu=0.05), dict(lr=1.0), "local", 0),
     ("FedDF", dict(global_epochs=2), dict(lr=0.05), "synthetic", 100),
+    ("AdaBest", dict(mu=0.02, beta=0.6), dict(lr=1.0), "local", 0),
+    ("FedDyn", dict(alpha=0.05), dict(lr=1.0), "local", 0),
 ]
 
 
@@ -68,17 +70,25 @@ def run(R, name, alg_kwargs, opt_kwargs, client, valid_size):
 
 
 # one client's send_to_server on CPU (local SGD; FedProx adds its proximal
-# gradient term): (algorithm, alg kwargs, client id, rounds, local SGD kwargs)
+# gradient term, AdaBest / FedDyn their drift terms and client-side h):
+# (algorithm, alg kwargs, client id, rounds, local SGD kwargs); a tuple of
+# rounds calls send_to_server once per entry on the same client storage, so
+# the second call sees the h the first one left (adabest.py:141-147,
+# feddyn.py:150-154)
 CLIENT_RUNS = [
     ("FedAvg", dict(), 3, 0, dict(lr=0.1)),
     ("FedProx", dict(mu=0.5), 3, 0, dict(lr=0.1)),
     ("FedProx", dict(mu=0.05), 11, 2, dict(lr=0.05, momentum=0.9)),
+    ("AdaBest", dict(mu=0.5, beta=0.6), 5, (1, 4), dict(lr=0.1)),
+    ("FedDyn", dict(alpha=0.5), 7, (0, 1), dict(lr=0.1)),
 ]
 
 
 def client_run(R, name, alg_kwargs, cid, rounds, local_opt):
     """Server init + send_to_client + the client's send_to_server, as
     _send_to_server (centralized_fl_algorithm.py:316-345) wires them."""
+    if isinstance(rounds, tuple):
+        return client_run_multi(R, name, alg_kwargs, cid, rounds, local_opt)
     torch.manual_seed(S.TORCH_SEED)
     dm = S.TensorDataManager()
     alg = R[name](
@@ -97,6 +107,36 @@ def client_run(R, name, alg_kwargs, cid, rounds, local_opt):
         scores_mod.CrossEntropyScore(), 32, 64, partial(torch.optim.SGD, **local_opt),
         None, "cpu", ctx=ctx)
     out = dict(local_params=msg["local_params"].detach().numpy().copy())
+    meta = dict(num_steps=msg["num_steps"], diverged=msg["diverged"],
+                num_samples=msg["num_samples"], metrics=msg["metrics"])
+    return out, meta
+
+
+def client_run_multi(R, name, alg_kwargs, cid, rounds_seq, local_opt):
+    """Successive send_to_server calls of one client with a persistent client
+    Storage; records the last message and the client's final h."""
+    torch.manual_seed(S.TORCH_SEED)
+    dm = S.TensorDataManager()
+    alg = R[name](
+        data_manager=dm, metric_logger=None, num_clients=S.NUM_CLIENTS,
+        sample_scheme="uniform", sample_rate=S.SAMPLE_RATE, model_def=S.TinyModel, epochs=2,
+        criterion_def="CrossEntropyScore", local_optimizer_def=partial(torch.optim.SGD,
+                                                                       **local_opt),
+        device="cpu", **alg_kwargs,
+    )
+    st = alg.get_server_storage()
+    storage_cls = __import__("importlib").import_module("fedsim.utils").Storage
+    scores_mod = __import__("importlib").import_module("fedsim.scores")
+    cstore = storage_cls()
+    for i, rounds in enumerate(rounds_seq):
+        ctx = R[name].send_to_client(st, cid)
+        torch.manual_seed(1000 + cid + 17 * i)
+        msg = R[name].send_to_server(
+            cid, rounds, cstore, dm.get_local_dataset(cid), "train", {}, 2,
+            scores_mod.CrossEntropyScore(), 32, 64, partial(torch.optim.SGD, **local_opt),
+            None, "cpu", ctx=ctx)
+    out = dict(local_params=msg["local_params"].detach().numpy().copy(),
+               h=cstore.read("h").detach().numpy().copy())
     meta = dict(num_steps=msg["num_steps"], diverged=msg["diverged"],
                 num_samples=msg["num_samples"], metrics=msg["metrics"])
     return out, meta
@@ -122,8 +162,10 @@ def main():
     for i, (name, akw, cid, rounds, lopt) in enumerate(CLIENT_RUNS):
         out, meta = client_run(R, name, akw, cid, rounds, lopt)
         rid = f"c{i}"
-        arrays[f"{rid}/local_params"] = out["local_params"]
-        clients.append(dict(id=rid, algorithm=name, alg_kwargs=akw, client_id=cid, rounds=rounds,
+        for k, v in out.items():
+            arrays[f"{rid}/{k}"] = v
+        clients.append(dict(id=rid, algorithm=name, alg_kwargs=akw, client_id=cid,
+                            rounds=list(rounds) if isinstance(rounds, tuple) else rounds,
                             local_opt=lopt, sha256=V.sha256(out["local_params"]), **meta))
         print(rid, name, akw, meta["num_steps"], meta["metrics"])
     gd = os.path.join(REPO, "tests", "golden")
