@@ -7,6 +7,8 @@
 * ``AppendixAggregator`` — the keep-every-value aggregator FedDF uses.
 * ``Storage`` — server / client key-value memory with access protection.
 * parameter packing (``vectorize_module`` ...) — flat fp32 vectors and views.
+* ``set_seed`` / ``get_from_module`` — the reference's seeding and lookup
+  helpers.
 """
 from .aggregators import AppendixAggregator, DeviceAggregator, SerialAggregator
 from .convert_parameters import (
@@ -14,12 +16,14 @@ from .convert_parameters import (
     vector_to_named_parameters_like,
     vector_to_parameters_like,
     vectorize_module,
+    vectorize_module_grads,
 )
 from .dict_ops import apply_on_dict
+from .misc import get_from_module, set_seed
 from .storage import Storage
 
 __all__ = [
     "SerialAggregator", "DeviceAggregator", "AppendixAggregator", "Storage", "apply_on_dict",
-    "vectorize_module", "initialize_module", "vector_to_parameters_like",
-    "vector_to_named_parameters_like",
+    "vectorize_module", "vectorize_module_grads", "initialize_module",
+    "vector_to_parameters_like", "vector_to_named_parameters_like", "get_from_module", "set_seed",
 ]

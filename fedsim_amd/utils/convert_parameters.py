@@ -53,3 +53,24 @@ def initialize_module(module: Module, vec: Tensor, clone=True, detach=True) -> b
         return False
     vector_to_parameters(vec, module.parameters())
     return True
+
+
+def vectorize_module_grads(module: Module, clone=True, detach=True):
+    """Gradients of ``module.parameters()`` packed like ``vectorize_module``
+    (reference: convert_parameters.py:97-126); None if any parameter has no
+    gradient yet.  Parameters on different devices raise TypeError, as
+    torch's parameters_to_vector does."""
+    grads = []
+    for p in module.parameters():
+        if p.grad is None:
+            return None
+        grads.append(p.grad)
+    if grads and any(g.device != grads[0].device for g in grads):
+        raise TypeError("Found two parameters on different devices, this is currently "
+                        "not supported.")
+    vec = torch.cat([g.reshape(-1) for g in grads]) if grads else torch.empty(0)
+    if clone:
+        vec = vec.clone()
+    if detach:
+        vec = vec.detach()
+    return vec

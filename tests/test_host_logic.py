@@ -285,3 +285,32 @@ def test_algorithm_registry_resolves_reference_names():
         assert cls.__name__ == name
     with pytest.raises(ValueError):
         training.get_algorithm("FedSGD")
+
+
+def test_vectorize_module_grads_and_misc_helpers():
+    """vectorize_module_grads (convert_parameters.py:97-126): None until every
+    parameter has a gradient, then the gradients packed in parameter order;
+    set_seed / get_from_module (random_utils.py, import_utils.py)."""
+    import random
+
+    import numpy as np
+    import torch
+
+    from fedsim_amd.utils import get_from_module, set_seed, vectorize_module_grads
+
+    m = torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Linear(4, 2))
+    assert vectorize_module_grads(m) is None
+    m(torch.randn(5, 3)).sum().backward()
+    want = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    got = vectorize_module_grads(m)
+    assert torch.equal(got, want) and got.data_ptr() != want.data_ptr()
+    m[1].bias.grad = None
+    assert vectorize_module_grads(m) is None
+
+    set_seed(5, use_cuda=False)
+    a = (np.random.rand(), random.random(), torch.rand(1).item())
+    set_seed(5, use_cuda=False)
+    assert a == (np.random.rand(), random.random(), torch.rand(1).item())
+
+    assert get_from_module("fedsim_amd.utils", "Storage").__name__ == "Storage"
+    assert get_from_module("fedsim_amd.utils", "nope") is None
