@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--step", default="fused", choices=["fused", "split"],
                     help="fused: server step inside the reduce pass (the product path); "
                          "split: reduce + divide, then a separate epilogue launch")
+    ap.add_argument("--mapping", default="auto", choices=["auto", "wide", "narrow1", "narrow2"],
+                    help="column mapping of the reduce kernel (include/fedagg.h "
+                         "FEDAGG_MAP_*); auto = the library's choice for P")
     ap.add_argument("--no-epilogue", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,13 +118,16 @@ def make_inputs(K, P, rank, dev, layout, C):
     return X, weights
 
 
-def load_pmc(path, K, P, flags, layout, step):
+def load_pmc(path, K, P, kernel, layout, step):
+    """HBM bytes per launch from the committed PMC summary
+    (tools/pmc_traffic.py), when it was measured on this exact kernel and
+    workload; else None."""
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("K") == K and d.get("P") == P and d.get("flags") == flags and \
+    if d.get("K") == K and d.get("P") == P and d.get("kernel") == kernel and \
             d.get("layout", "strided") == layout and d.get("step", "split") == step:
         return d.get("hbm_bytes_per_launch")
     return None
@@ -172,7 +178,7 @@ def main():
     dev = torch.device("cuda", local)
     K, P = a.K, a.P
     flags = ops.tuning_flags(unroll=a.unroll, vpt=a.vpt if a.layout == "strided" else 0,
-                             nt=bool(a.nt))
+                             nt=bool(a.nt), mapping=a.mapping)
     fused = a.step == "fused" and a.layout == "blocked" and not a.no_epilogue
     step_mode = "fused" if fused else "split"
     X, weights = make_inputs(K, P, rank, dev, a.layout, a.C)
@@ -188,7 +194,7 @@ def main():
 
     def reduce():
         if fused:
-            ops.reduce_blocked_step(X, w32, sstep, W=W)
+            ops.reduce_blocked_step(X, w32, sstep, W=W, mapping=a.mapping)
         elif a.layout == "strided":
             ops.reduce_slab(X[:, :P], w32, avg, W=W, P=P, flags=flags)
         else:
@@ -230,7 +236,13 @@ def main():
     # grad write; split (reduce kernel alone) = the average's write
     alg_bytes_launch = 4.0 * K * P + 4.0 * K + (12.0 * P if fused else 4.0 * P)
     achieved = alg_bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_pmc(a.pmc_json, K, P, flags,
+    # the kernel the library launched: the fused step path takes only the
+    # mapping bits, the plain reduce all of `flags`
+    mapping, unroll = ops.column_mapping(
+        P, ops.tuning_flags(mapping=a.mapping) if fused else flags)
+    kernel = ("k_reduce_vec" if mapping == "wide" else
+              f"k_reduce_narrow<U={unroll}, VW={mapping[-1]}>")
+    traffic = load_pmc(a.pmc_json, K, P, kernel,
                        a.layout if a.layout == "strided" else f"blocked{a.C}", step_mode)
     result = {
         "metric": METRIC,
@@ -257,11 +269,12 @@ def main():
             "parallelism": f"param-shard{world}" if world > 1 else "single",
             "mode": "exact (bitwise vs reference CPU)",
             "layout": a.layout if a.layout == "strided" else f"blocked C={a.C}",
+            "mapping": mapping if mapping == "wide" else f"{mapping} (U={unroll})",
             "flags": flags,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_reduce_vec (%s)" % (
+            "kernel": "%s (%s)" % (kernel,
                 "fedagg_reduce_step_blocked_f32, EpiStep<FEDAVG>" if fused else
                 "fedagg_reduce_blocked_f32" if a.layout == "blocked" else "fedagg_reduce_f32"),
             "achieved": round(achieved, 1),

@@ -33,6 +33,7 @@ FEDAGG_VPT_SHIFT = 12
 FEDAGG_BS_SHIFT = 14
 FEDAGG_FLAT = 0x10000
 FEDAGG_LDSW = 0x20000
+FEDAGG_MAP_SHIFT = 18
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0
@@ -74,6 +75,11 @@ class StepArgs(ctypes.Structure):
 SIGNATURES = {
     "fedagg_abi_version": (ctypes.c_int, []),
     "fedagg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "fedagg_column_mapping": (
+        ctypes.c_int,
+        [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+         ctypes.POINTER(ctypes.c_int)],
+    ),
     "fedagg_reduce_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,

@@ -55,6 +55,15 @@ constexpr int kDefaultBsSel = 1;   // blocked layout: 256-lane workgroups
 constexpr int kRowsUnroll = 4;     // row-pointer fused step (fedagg_reduce_step_rows_f32)
 constexpr int kRowsVpt = 2;
 constexpr int kWeightTile = 2048;  // FEDAGG_LDSW ablation: weights per LDS tile
+// Default column mapping = narrow (tools/sweep_mapping.py, tools/ab_mapping.py,
+// profiles/r01r/, r01t/, interleaved A/B on MI355X):
+//  * P < 2^20: one column per lane, U = 8.  The f32x4-slot kernels cannot fill
+//    256 CUs there (P = 199,210: 6.1 vs 1.3 TB/s at K = 1000);
+//  * P >= 2^20: two columns per lane, U = 16 (U = 8 from 2^24 on), even with
+//    or ahead of the tuned f32x4 kernels: +1.3 % at 1000 x 25 M, +3.8 % at
+//    1000 x 6.25 M, +5.7 % at 10,000 x 3.125 M (config 4's shard).
+constexpr int64_t kNarrowWideP = int64_t(1) << 20;
+constexpr int64_t kNarrowLongP = int64_t(1) << 24;
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).
@@ -267,8 +276,9 @@ __device__ __forceinline__ StepOut step_math(float a, float c, float x, float b,
 // ---------------------------------------------------------------------------
 struct EpiStore {  // plain reduce: store it
   float* out;
-  __device__ __forceinline__ void vec(int64_t off, f32x4 a) const {
-    *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(out) + off) = a;
+  template <class V>  // f32x4 / f32x2 columns at byte offset `off`
+  __device__ __forceinline__ void vec(int64_t off, V a) const {
+    *reinterpret_cast<V*>(reinterpret_cast<char*>(out) + off) = a;
   }
   __device__ __forceinline__ void one(int64_t col, float a) const { out[col] = a; }
 };
@@ -302,17 +312,19 @@ struct EpiStep {  // server step on the average, in registers
     if constexpr (MOM) p.buf[i] = o.buf;
     p.cloud[i] = o.cloud;
   }
-  __device__ __forceinline__ void vec(int64_t off, f32x4 a) const {
+  template <class V>  // f32x4 / f32x2 columns at byte offset `off`
+  __device__ __forceinline__ void vec(int64_t off, V a) const {
+    constexpr int N = sizeof(V) / sizeof(float);
     auto at = [off](float* q) {
-      return reinterpret_cast<f32x4*>(reinterpret_cast<char*>(q) + off);
+      return reinterpret_cast<V*>(reinterpret_cast<char*>(q) + off);
     };
-    const f32x4 c = *at(p.cloud);
-    f32x4 x = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    const V c = *at(p.cloud);
+    V x = {}, b = {};
     if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) x = *at(p.aux);
     if constexpr (MOM) b = *at(p.buf);
-    f32x4 nc, g, nx, nb;
+    V nc, g, nx, nb;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < N; ++e) {
       const StepOut o = step_math<ALGO, MOM>(a[e], c[e], x[e], b[e], p.coef, p.sa);
       nc[e] = o.cloud;
       g[e] = o.g;
@@ -459,18 +471,157 @@ __global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
     reduce_scalar_cols<NT>(rows, w, B, nvec * 4 + threadIdx.x, acc_in, epi, W32, flags);
 }
 
-// Generic path for rows that are not 16-byte aligned: one column per lane,
-// 4-byte coalesced loads (256 B per wave-instruction).  Same arithmetic.
-template <class Rows>
-__global__ __launch_bounds__(kBlock) void k_reduce_scalar(Rows rows,
-                                                          const float* __restrict__ w,
+
+// ---------------------------------------------------------------------------
+// Narrow mapping for small P: VW (1 or 2) columns per lane instead of f32x4
+// slots.  VW = 1 is also the path for rows that are not 16-byte aligned.    An in-order per-column sum has no parallelism but its columns, so
+// at the reference's model sizes (SimpleMLP P = 199,210: 49,802 f32x4 slots =
+// 778 waves, under one per SIMD) the wide kernel leaves most of the chip idle.
+// One column per lane gives P lanes (3,113 waves there); U rows of dword loads
+// stay in flight per lane.  Same per-element arithmetic and order.
+// ---------------------------------------------------------------------------
+using f32x2 = float __attribute__((ext_vector_type(2)));
+using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
+
+template <int VW>
+struct Cols {
+  float v[VW];
+};
+
+template <int VW, bool NT>
+__device__ __forceinline__ Cols<VW> buf_load_cols(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                                  uint32_t soff) {
+  Cols<VW> o;
+  if constexpr (VW == 1) {
+    o.v[0] = __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff),
+                                                    static_cast<int>(soff), NT ? 2 : 0));
+  } else {
+    const f32x2 t = __builtin_bit_cast(
+        f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(voff),
+                                                    static_cast<int>(soff), NT ? 2 : 0));
+    o.v[0] = t.x;
+    o.v[1] = t.y;
+  }
+  return o;
+}
+
+// Column-blocked slab: the workgroup's 256*VW columns lie in one column block
+// b (C is a multiple of 256*VW); its region is one buffer descriptor, the row
+// an SGPR soffset, the lane's column-in-block a VGPR voffset.
+struct NarrowBlocked {
+  const float* X;
+  int64_t Kcap;
+  int64_t C;
+  template <int VW>
+  __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
+    return static_cast<uint32_t>(c & (C - 1)) * 4u;
+  }
+  template <int VW, bool NT>
+  __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
+    const int64_t b = (static_cast<int64_t>(blockIdx.x) * kBlock * VW) >> __builtin_ctzll(C);
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(X + b * Kcap * C), static_cast<short>(0),
+        static_cast<int>(static_cast<uint32_t>(Kcap * C * 4)), 0x00020000);
+    return buf_load_cols<VW, NT>(r, voff, static_cast<uint32_t>(k) * static_cast<uint32_t>(C * 4));
+  }
+};
+
+// Row-pointer table: one descriptor per row (wave-uniform scalar load).
+struct NarrowTable {
+  const float* const* rows;
+  uint32_t row_bytes;
+  template <int VW>
+  __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
+    return static_cast<uint32_t>(c) * 4u;
+  }
+  template <int VW, bool NT>
+  __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(rows[k]), static_cast<short>(0), static_cast<int>(row_bytes),
+        0x00020000);
+    return buf_load_cols<VW, NT>(r, voff, 0u);
+  }
+};
+
+// Row-major [B, ldx] slab (may exceed a descriptor's 4 GiB range): flat loads.
+struct NarrowStrided {
+  const float* X;
+  int64_t ldx;
+  template <int VW>
+  __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
+    return static_cast<uint32_t>(c) * 4u;
+  }
+  template <int VW, bool NT>
+  __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
+    const char* p = reinterpret_cast<const char*>(X + k * ldx) + voff;
+    Cols<VW> o;
+    if constexpr (VW == 1) {
+      o.v[0] = ld1<NT>(p, 0);
+    } else {
+      const f32x2* q = reinterpret_cast<const f32x2*>(p);
+      const f32x2 t = NT ? __builtin_nontemporal_load(q) : *q;
+      o.v[0] = t.x;
+      o.v[1] = t.y;
+    }
+    return o;
+  }
+};
+
+template <int U, int VW, bool NT, class NR, class Epi>
+__global__ __launch_bounds__(kBlock) void k_reduce_narrow(NR rows, const float* __restrict__ w,
                                                           int64_t B, int64_t P,
-                                                          const float* acc_in,
-                                                          float* out, float W32,
-                                                          int flags) {
-  const int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (c >= P) return;
-  reduce_scalar_cols<false>(rows, w, B, c, acc_in, EpiStore{out}, W32, flags);
+                                                          const float* acc_in, Epi epi,
+                                                          float W32, int flags) {
+  const int64_t c0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * VW;
+  const bool ok = c0 < P;
+  const int64_t c = ok ? c0 : P - VW;  // clamp: load something valid, store nothing
+  const uint32_t voff = rows.template lane_off<VW>(c);
+  float a[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) a[e] = (flags & FEDAGG_INIT) ? 0.f : acc_in[c + e];
+  int64_t k = 0;
+  for (; k + U <= B; k += U) {
+    Cols<VW> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = rows.template load<VW, NT>(k + u, voff);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wk = w[k + u];
+#pragma unroll
+      for (int e = 0; e < VW; ++e) a[e] = axpy_rn(a[e], v[u].v[e], wk);
+    }
+  }
+  if (k < B) {
+    // the last B % U rows: one load per lane per row, so a plain tail loop
+    // would wait out a full memory latency per row (what small-K rounds are
+    // made of); issue them all before the in-order adds, under wave-uniform
+    // guards
+    const int64_t rem = B - k;
+    Cols<VW> v[U - 1];
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (u < rem) v[u] = rows.template load<VW, NT>(k + u, voff);
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u) {
+      if (u < rem) {
+        const float wk = w[k + u];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) a[e] = axpy_rn(a[e], v[u].v[e], wk);
+      }
+    }
+  }
+  if (flags & FEDAGG_FINALIZE) {
+#pragma unroll
+    for (int e = 0; e < VW; ++e) a[e] = a[e] / W32;
+  }
+  if (ok) {
+    if constexpr (VW == 2) {
+      epi.vec(c0 * 4, f32x2{a[0], a[1]});
+    } else {
+      epi.one(c0, a[0]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -671,16 +822,8 @@ hipError_t dispatch_nt(const Rows& rows, const float* w, int64_t B, int64_t P,
 }
 
 template <class Rows>
-hipError_t dispatch_reduce(const Rows& rows, bool vec_ok, const float* w, int64_t B,
-                           int64_t P, const float* acc_in, float* out, float W32,
-                           int flags, hipStream_t s) {
-  if (!vec_ok) {
-    int64_t grid = (P + kBlock - 1) / kBlock;
-    if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_reduce_scalar<Rows>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
-                       0, s, rows, w, B, P, acc_in, out, W32, flags);
-    return hipGetLastError();
-  }
+hipError_t dispatch_reduce(const Rows& rows, const float* w, int64_t B, int64_t P,
+                           const float* acc_in, float* out, float W32, int flags, hipStream_t s) {
   const int vpt_sel = (flags & FEDAGG_VPT_MASK) >> FEDAGG_VPT_SHIFT;
   switch (vpt_sel == 0 ? kDefaultVptSel : vpt_sel) {
     case 1: return dispatch_nt<kBlock, 1>(rows, w, B, P, acc_in, out, W32, flags, s);
@@ -722,10 +865,84 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (B > 0 && !w) return FEDAGG_EINVAL;
   if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
-                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW))
+                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_MAP_MASK))
     return FEDAGG_EINVAL;
   return 0;
 }
+
+// Columns per lane of the narrow mapping for this call, or 0 for the wide
+// (f32x4-slot) kernels.  `vw_ok` says whether 2 columns per lane are possible
+// (P even, 8-byte aligned operands).
+int narrow_vw(int flags, int64_t P, bool vw2_ok) {
+  const int m = (flags & FEDAGG_MAP_MASK) >> FEDAGG_MAP_SHIFT;
+  int vw;
+  if (m == 1) return 0;
+  if (m == 2) vw = 1;
+  else if (m == 3) vw = 2;
+  else vw = P < kNarrowWideP ? 1 : 2;
+  return (vw == 2 && !vw2_ok) ? 1 : vw;
+}
+
+template <int U, int VW, bool NT, class NR, class Epi>
+hipError_t launch_narrow_t(const NR& rows, const float* w, int64_t B, int64_t P,
+                           const float* acc_in, const Epi& epi, float W32, int flags,
+                           hipStream_t s) {
+  const int64_t grid = (P + kBlock * VW - 1) / (kBlock * VW);
+  hipLaunchKernelGGL((k_reduce_narrow<U, VW, NT, NR, Epi>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kBlock), 0, s, rows, w, B, P, acc_in, epi, W32, flags);
+  return hipGetLastError();
+}
+
+// Narrow k-unroll: selector 2 / 3 / 5 = 8 / 16 / 32, anything else = the
+// per-P default.
+int narrow_unroll(int flags, int64_t P) {
+  switch ((flags & FEDAGG_UNROLL_MASK) >> FEDAGG_UNROLL_SHIFT) {
+    case 2: return 8;
+    case 3: return 16;
+    case 5: return 32;
+    default: return (P < kNarrowWideP || P >= kNarrowLongP) ? 8 : 16;
+  }
+}
+
+template <int VW, bool NT, class NR, class Epi>
+hipError_t launch_narrow_u(const NR& rows, const float* w, int64_t B, int64_t P,
+                           const float* acc_in, const Epi& epi, float W32, int flags,
+                           hipStream_t s) {
+  switch (narrow_unroll(flags, P)) {
+    case 8: return launch_narrow_t<8, VW, NT>(rows, w, B, P, acc_in, epi, W32, flags, s);
+    case 32: return launch_narrow_t<32, VW, NT>(rows, w, B, P, acc_in, epi, W32, flags, s);
+    default: return launch_narrow_t<16, VW, NT>(rows, w, B, P, acc_in, epi, W32, flags, s);
+  }
+}
+
+// Plain reduce (EpiStore): NT from the flags.
+template <class NR>
+hipError_t launch_narrow_store(const NR& rows, int vw, const float* w, int64_t B, int64_t P,
+                               const float* acc_in, float* out, float W32, int flags,
+                               hipStream_t s) {
+  const EpiStore st{out};
+  const bool nt = (flags & FEDAGG_NT) != 0;
+  if (vw == 2)
+    return nt ? launch_narrow_u<2, true>(rows, w, B, P, acc_in, st, W32, flags, s)
+              : launch_narrow_u<2, false>(rows, w, B, P, acc_in, st, W32, flags, s);
+  return nt ? launch_narrow_u<1, true>(rows, w, B, P, acc_in, st, W32, flags, s)
+            : launch_narrow_u<1, false>(rows, w, B, P, acc_in, st, W32, flags, s);
+}
+
+// Fused server step: non-temporal row loads.
+template <class NR, class Epi>
+hipError_t launch_narrow_step(const NR& rows, int vw, const float* w, int64_t B, int64_t P,
+                              const float* acc_in, const Epi& epi, float W32, int flags,
+                              hipStream_t s) {
+  return vw == 2 ? launch_narrow_u<2, true>(rows, w, B, P, acc_in, epi, W32, flags, s)
+                 : launch_narrow_u<1, true>(rows, w, B, P, acc_in, epi, W32, flags, s);
+}
+
+inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+
+// Column-block widths the blocked kernels are built for (one workgroup's span
+// of the wide mapping; a multiple of the narrow mapping's 256 * 2 columns).
+inline bool valid_block_cols(int64_t C) { return C == 1024 || C == 2048 || C == 4096; }
 
 // Validate a server step's operands and pack them for EpiStep.
 int make_step(int algo, float coef, float* cloud, float* aux, float* avg_prev, float* buf,
@@ -777,6 +994,13 @@ extern "C" {
 
 int fedagg_abi_version(void) { return FEDAGG_ABI_VERSION; }
 
+int fedagg_column_mapping(int64_t P, int flags, int vw2_ok, int* vw, int* unroll) {
+  if (P < 0 || !vw || !unroll) return FEDAGG_EINVAL;
+  *vw = narrow_vw(flags, P, vw2_ok != 0);
+  *unroll = *vw ? narrow_unroll(flags, P) : 0;
+  return 0;
+}
+
 const char* fedagg_strerror(int code) {
   if (code == 0) return "success";
   if (code == FEDAGG_EINVAL) return "fedagg: invalid argument";
@@ -790,11 +1014,17 @@ int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B, in
   int rc = check_reduce_args(w, B, P, acc_in, out, flags);
   if (rc != 0 || P == 0) return rc;
   if (B > 0 && (!X || ldx < P)) return FEDAGG_EINVAL;
+  const bool init = (flags & FEDAGG_INIT) != 0;
   const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(X) && (ldx % 4 == 0) &&
-                      aligned16(out) && ((flags & FEDAGG_INIT) || aligned16(acc_in));
-  RowsStrided rows{X, ldx};
-  return static_cast<int>(dispatch_reduce(rows, vec_ok, w, B, P, acc_in, out, W32, flags,
-                                          static_cast<hipStream_t>(stream)));
+                      aligned16(out) && (init || aligned16(acc_in));
+  const bool vw2_ok = !(flags & FEDAGG_SCALAR) && P % 2 == 0 && aligned8(X) && ldx % 2 == 0 &&
+                      aligned8(out) && (init || aligned8(acc_in));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // misaligned rows take the one-column-per-lane kernel whatever the mapping
+  const int vw = vec_ok ? narrow_vw(flags, P, vw2_ok) : 1;
+  if (vw) return static_cast<int>(launch_narrow_store(NarrowStrided{X, ldx}, vw, w, B, P, acc_in,
+                                                      out, W32, flags, s));
+  return static_cast<int>(dispatch_reduce(RowsStrided{X, ldx}, w, B, P, acc_in, out, W32, flags, s));
 }
 
 int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, int64_t P,
@@ -805,15 +1035,20 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
   if (B > 0 && !rows) return FEDAGG_EINVAL;
   // The table lives in device memory and cannot be inspected here without a
   // sync: the caller passes FEDAGG_SCALAR unless every rows[k] is 16-B aligned.
-  const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(out) &&
-                      ((flags & FEDAGG_INIT) || aligned16(acc_in));
+  const bool init = (flags & FEDAGG_INIT) != 0;
+  const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(out) && (init || aligned16(acc_in));
+  // 16-B aligned rows (no FEDAGG_SCALAR) are 8-B aligned too
+  const bool vw2_ok = vec_ok && P % 2 == 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int vw = vec_ok ? narrow_vw(flags, P, vw2_ok) : 1;
+  if (vw)
+    return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B, P,
+                                                acc_in, out, W32, flags, s));
   // buffer-descriptor loads unless asked for flat 64-bit addressing
   if (flags & FEDAGG_FLAT)
-    return static_cast<int>(
-        dispatch_reduce(RowsTable{rows}, vec_ok, w, B, P, acc_in, out, W32, flags, s));
-  return static_cast<int>(dispatch_reduce(RowsTableBuf{rows, table_row_bytes(P)}, vec_ok, w, B, P,
-                                          acc_in, out, W32, flags, s));
+    return static_cast<int>(dispatch_reduce(RowsTable{rows}, w, B, P, acc_in, out, W32, flags, s));
+  return static_cast<int>(dispatch_reduce(RowsTableBuf{rows, table_row_bytes(P)}, w, B, P, acc_in,
+                                          out, W32, flags, s));
 }
 
 int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
@@ -822,15 +1057,22 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   int rc = check_reduce_args(w, B, P, acc_in, out, flags);
   if (rc != 0 || P == 0) return rc;
   if (B > Kcap || (B > 0 && !Xb)) return FEDAGG_EINVAL;
+  if (!valid_block_cols(C)) return FEDAGG_EINVAL;
   if (!aligned16(Xb) || !aligned16(out) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in)))
     return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   int bs_sel = (flags & FEDAGG_BS_MASK) >> FEDAGG_BS_SHIFT;
   if (bs_sel == 0) bs_sel = kDefaultBsSel;
   hipError_t e;
+  const bool region32 = Kcap * C * 4 < (int64_t(1) << 32);
+  const int vw = (flags & (FEDAGG_LDSW | FEDAGG_FLAT)) || !region32
+                     ? 0
+                     : narrow_vw(flags, P, P % 2 == 0 && ((flags & FEDAGG_INIT) || aligned8(acc_in)));
   // buffer-descriptor path unless asked for flat loads or a block region is
   // too large for a 32-bit descriptor range
-  if (flags & FEDAGG_LDSW) {
+  if (vw) {
+    e = launch_narrow_store(NarrowBlocked{Xb, Kcap, C}, vw, w, B, P, acc_in, out, W32, flags, s);
+  } else if (flags & FEDAGG_LDSW) {
     // ablation: only the default configuration (C=4096, 256 lanes, U=4, nt)
     if (C != 4096 || Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
     e = launch_vec<256, 4, 4, true, RowsBlockedBuf, true>(RowsBlockedBuf{Xb, Kcap, C}, w, B, P,
@@ -953,14 +1195,20 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
   if (rc != 0 || P == 0) return rc;
   if (flags & (FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
   if (B > Kcap || (B > 0 && !Xb)) return FEDAGG_EINVAL;
+  if (!valid_block_cols(C)) return FEDAGG_EINVAL;
   if (Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
   if (!aligned16(Xb) || !step_aligned(sp) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in)))
     return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const RowsBlockedBuf rows{Xb, Kcap, C};
+  const int vw = narrow_vw(flags, P, P % 2 == 0);
   // the per-C default configuration of fedagg_reduce_blocked_f32 (256 lanes,
-  // VPT = C/1024, U = 4 at C=4096 else 2, non-temporal loads)
+  // VPT = C/1024, U = 4 at C=4096 else 2, non-temporal loads), or the narrow
+  // mapping at small P
   hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+    if (vw)
+      return launch_narrow_step(NarrowBlocked{Xb, Kcap, C}, vw, w, B, P, acc_in, epi, W32, flags,
+                                s);
     switch (C) {
       case 4096: return launch_vec<256, 4, 4, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
                                                                           epi, W32, flags, s);
@@ -995,6 +1243,15 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   // per lane, U = kRowsUnroll); the rows are the caller's separate
   // allocations, read through buffer descriptors unless FEDAGG_FLAT
   const bool nt = (flags & FEDAGG_NT) != 0;
+  const int vw = narrow_vw(flags, P, P % 2 == 0);
+  if (vw) {
+    const NarrowTable tab{rows, table_row_bytes(P)};
+    hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+      return launch_narrow_step(tab, vw, w, B, P, acc_in, epi, W32, flags, s);
+    });
+    if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
+    return static_cast<int>(e);
+  }
   auto go = [&](const auto& tab) {
     using T = std::decay_t<decltype(tab)>;
     return with_step(step->algo, mom, sp, [&](auto epi) {

@@ -40,17 +40,21 @@ def fl32(x) -> float:
 
 
 def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
-                 flat: bool = False, ldsw: bool = False) -> int:
+                 flat: bool = False, ldsw: bool = False, mapping: str = "auto") -> int:
     """Kernel tuning bits (include/fedagg.h): k-unroll, float4 slots per lane
     (row-major / pointer-table layouts), non-temporal loads, the workgroup
-    size of the column-blocked layout, and flat (instead of buffer-descriptor)
-    loads for it.  0 / False = library default."""
-    sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4}[unroll]
+    size of the column-blocked layout, flat (instead of buffer-descriptor)
+    loads for it, and the column mapping (``"auto"``, ``"wide"`` = f32x4
+    slots, ``"narrow1"`` / ``"narrow2"`` = one / two columns per lane).
+    0 / False / "auto" = library default."""
+    sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4, 32: 5}[unroll]
+    msel = {"auto": 0, "wide": 1, "narrow1": 2, "narrow2": 3}[mapping]
     vsel = {0: 0, 1: 1, 2: 2, 4: 3}[vpt]
     bsel = {0: 0, 256: 1, 512: 2, 1024: 3}[bs]
     return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
             | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0)
-            | (_native.FEDAGG_FLAT if flat else 0) | (_native.FEDAGG_LDSW if ldsw else 0))
+            | (_native.FEDAGG_FLAT if flat else 0) | (_native.FEDAGG_LDSW if ldsw else 0)
+            | (msel << _native.FEDAGG_MAP_SHIFT))
 
 
 # Tuned defaults for the column-blocked reduce (profiles/r01_sweep*/: K=1000 at
@@ -60,6 +64,16 @@ DEFAULT_FLAGS = tuning_flags(unroll=4, nt=True)
 _FLAGS_BY_C = {4096: tuning_flags(unroll=4, nt=True), 2048: tuning_flags(unroll=2, nt=True),
                1024: tuning_flags(unroll=2, nt=True)}
 _MIN_WORKGROUPS = 2048  # ~8 per CU: below this, narrower column blocks win
+
+
+def column_mapping(P: int, flags: int = 0, vw2_ok: bool = True):
+    """The reduce kernel the library picks for P columns under ``flags``
+    (fedagg_column_mapping): ``("wide", None)`` for the f32x4-slot kernels,
+    else ``("narrow<vw>", unroll)``."""
+    vw, u = ctypes.c_int(), ctypes.c_int()
+    check(_native.load().fedagg_column_mapping(P, flags, int(vw2_ok), ctypes.byref(vw),
+                                                ctypes.byref(u)), "fedagg_column_mapping")
+    return ("wide", None) if vw.value == 0 else (f"narrow{vw.value}", u.value)
 
 
 def choose_block_cols(P: int) -> int:
@@ -407,9 +421,12 @@ def reduce_blocked_step(
     acc_in: Optional[torch.Tensor] = None,
     W: Optional[float] = None,
     r0: int = 0,
+    mapping: str = "auto",
+    unroll: int = 0,
 ) -> torch.Tensor:
     """reduce_blocked(..., out=avg) then step.apply(avg), fused into one pass
-    (fedagg_reduce_step_blocked_f32).  Returns step.cloud."""
+    (fedagg_reduce_step_blocked_f32).  Returns step.cloud.  ``mapping`` as in
+    :func:`tuning_flags` (same results)."""
     _require_hip_f32(Xb, "Xb")
     _require_hip_f32(w32, "w32")
     if Xb.dim() != 3 or not Xb.is_contiguous():
@@ -423,7 +440,7 @@ def reduce_blocked_step(
         raise ValueError("w32 too short")
     if r0 < 0 or B < 0 or r0 + B > Kcap:
         raise ValueError("row range outside the slab")
-    f = 0
+    f = tuning_flags(unroll=unroll, mapping=mapping)
     if acc_in is None:
         f |= FEDAGG_INIT
     else:
@@ -458,6 +475,8 @@ def reduce_rows_step(
     nt: bool = True,
     table: Optional[torch.Tensor] = None,
     flat: bool = False,
+    mapping: str = "auto",
+    unroll: int = 0,
 ) -> torch.Tensor:
     """reduce_rows(rows, ..., out=avg) then step.apply(avg), fused into one
     pass over the caller's own client tensors (fedagg_reduce_step_rows_f32):
@@ -477,7 +496,7 @@ def reduce_rows_step(
         raise ValueError("w32 too short")
     if not step.aligned():
         raise ValueError("every server-step operand must be 16-B aligned")
-    f = (FEDAGG_NT if nt else 0) | (_native.FEDAGG_FLAT if flat else 0)
+    f = (FEDAGG_NT if nt else 0) | tuning_flags(flat=flat, mapping=mapping, unroll=unroll)
     if acc_in is None:
         f |= FEDAGG_INIT
     else:

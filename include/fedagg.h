@@ -63,7 +63,8 @@ extern "C" {
 #define FEDAGG_FINALIZE  0x2  /* store fl32(acc / W32) instead of the raw sum              */
 #define FEDAGG_NT        0x4  /* non-temporal (streaming) loads of the client rows         */
 #define FEDAGG_SCALAR    0x8  /* force the 4-byte-per-lane path (rows not 16-B aligned)    */
-/* bits 8..11: k-unroll selector, 0 = library default, 1 = 4, 2 = 8, 3 = 16, 4 = 2 */
+/* bits 8..11: k-unroll selector, 0 = library default, 1 = 4, 2 = 8, 3 = 16, 4 = 2,
+ * 5 = 32 (narrow mapping only; it takes 2 / 3 / 5, anything else = default 16) */
 #define FEDAGG_UNROLL_SHIFT 8
 #define FEDAGG_UNROLL_MASK  0xF00
 /* bits 12..13: float4 slots per lane, 0 = library default, 1 = 1, 2 = 2, 3 = 4 */
@@ -80,6 +81,15 @@ extern "C" {
 /* ablation: stage the per-client weights through LDS tiles instead of reading
  * them with wave-uniform scalar loads (same results; A/B measurement switch) */
 #define FEDAGG_LDSW     0x20000
+/* bits 18..19: column mapping of the reduce kernels.  An in-order per-column
+ * sum is parallel over columns only, so at small P the f32x4-slot ("wide")
+ * kernels leave CUs idle (P = 199,210 is 778 waves).  0 = library default
+ * (narrow: one column per lane below P = 2^20, two from there on), 1 = wide
+ * (f32x4 slots; the unroll / VPT / BS tuning bits apply to it), 2 = narrow,
+ * one column per lane, 3 = narrow, two columns per lane (falls back to one
+ * when P is odd or an operand is not 8-byte aligned).  Same results. */
+#define FEDAGG_MAP_SHIFT 18
+#define FEDAGG_MAP_MASK  0xC0000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
@@ -90,6 +100,15 @@ int fedagg_abi_version(void);
 
 /* Human-readable message for a return code (static storage, never NULL). */
 const char* fedagg_strerror(int code);
+
+/*
+ * Which reduce kernel a call with these flags takes for P columns (host-side
+ * decision, no device access): *vw = columns per lane of the narrow mapping
+ * (1 or 2), or 0 for the wide f32x4-slot kernels; *unroll = the narrow
+ * kernel's k-unroll (0 when wide).  vw2_ok: whether two columns per lane are
+ * possible (P even, operands 8-byte aligned).
+ */
+int fedagg_column_mapping(int64_t P, int flags, int vw2_ok, int* vw, int* unroll);
 
 /*
  * Weighted sequential reduction of B client rows into one accumulator.
@@ -250,9 +269,10 @@ typedef struct fedagg_step_args {
  * It replaces SerialAggregator.pop (aggregators.py:104-122) followed by the
  * algorithm's optimize (fedavg.py:193-208, adabest.py:172-189,
  * feddyn.py:157-194), with bit-identical results to the two-call sequence.
- * Flags: FEDAGG_INIT / FEDAGG_FINALIZE as for the reduce. The tuning bits are
- * ignored (the per-C default configuration is used). FEDAGG_FLAT / FEDAGG_LDSW /
- * FEDAGG_SCALAR are rejected. Every [P] operand must be 16-byte aligned, and a
+ * Flags: FEDAGG_INIT / FEDAGG_FINALIZE as for the reduce; the column-mapping
+ * bits and, for the narrow mapping, the unroll selector apply (the wide
+ * mapping uses its per-C default configuration, non-temporal loads).
+ * FEDAGG_FLAT / FEDAGG_LDSW / FEDAGG_SCALAR are rejected. Every [P] operand must be 16-byte aligned, and a
  * column block's region (Kcap * C * 4 bytes) must be < 4 GiB.
  */
 int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,

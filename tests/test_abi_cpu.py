@@ -40,7 +40,8 @@ def lib():
 def test_header_declares_the_abi():
     fns = header_functions()
     assert fns == sorted([
-        "fedagg_abi_version", "fedagg_strerror", "fedagg_reduce_f32", "fedagg_reduce_rows_f32",
+        "fedagg_abi_version", "fedagg_strerror", "fedagg_column_mapping", "fedagg_reduce_f32",
+        "fedagg_reduce_rows_f32",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
@@ -62,7 +63,7 @@ def test_python_mirror_matches_header(lib):
     d = header_defines()
     assert _native.ABI_VERSION == d["FEDAGG_ABI_VERSION"] == lib.fedagg_abi_version()
     for name in ("FEDAGG_INIT", "FEDAGG_FINALIZE", "FEDAGG_NT", "FEDAGG_SCALAR",
-                 "FEDAGG_UNROLL_SHIFT", "FEDAGG_VPT_SHIFT", "FEDAGG_EINVAL"):
+                 "FEDAGG_UNROLL_SHIFT", "FEDAGG_VPT_SHIFT", "FEDAGG_MAP_SHIFT", "FEDAGG_EINVAL"):
         assert getattr(_native, name) == d[name], name
     assert set(_native.exported_symbols()) == set(header_functions())
 
@@ -150,3 +151,20 @@ def test_build_is_gfx950():
     else:
         assert "gfx950" in out
     assert ctypes.sizeof(ctypes.c_void_p) == 8
+
+
+def test_column_mapping_decision():
+    """fedagg_column_mapping: the library's default mapping per P (narrow, one
+    column per lane below 2^20, two from there on; unroll 8 / 16 / 8) and the
+    forced ones; host-side, no device needed."""
+    from fedsim_amd import ops
+
+    assert ops.column_mapping(199_210) == ("narrow1", 8)
+    assert ops.column_mapping(1_085_668) == ("narrow2", 16)
+    assert ops.column_mapping(25_000_000) == ("narrow2", 8)
+    assert ops.column_mapping(25_000_000, vw2_ok=False) == ("narrow1", 8)
+    assert ops.column_mapping(25_000_000, ops.tuning_flags(mapping="wide")) == ("wide", None)
+    assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow2", unroll=32)) == ("narrow2", 32)
+    assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow1", unroll=16)) == ("narrow1", 16)
+    # unroll selectors the narrow kernels do not build fall back to the default
+    assert ops.column_mapping(199_210, ops.tuning_flags(unroll=4)) == ("narrow1", 8)

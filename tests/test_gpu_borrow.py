@@ -184,3 +184,33 @@ def test_borrowed_full_size_round(dev):
     np.testing.assert_array_equal(bits(avg.index_select(0, cols).cpu().numpy()), bits(exp_avg))
     exp_cloud = ref.fedavg_sgd(exp_avg, np.zeros(4096, np.float32), 1.0)
     np.testing.assert_array_equal(bits(cloud.index_select(0, cols).cpu().numpy()), bits(exp_cloud))
+
+
+@pytest.mark.parametrize("P", [5, 70_001, 70_002])
+@pytest.mark.parametrize("mapping", ["wide", "narrow1", "narrow2"])
+@pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
+def test_rows_step_mappings_bitwise(algo, mapping, P, dev):
+    """fedagg_reduce_step_rows_f32 under each column mapping (two columns per
+    lane falls back to one for odd P) == the oracle's reduce + server step."""
+    from fedsim_amd import ops
+
+    K = 11
+    X = V.client_rows("realistic", K, P, 8)
+    w = V.client_weights("fedavg", K, 8)
+    W = sum(w)
+    avg = ref.reduce(X, w, W=W)
+    rows = [torch.from_numpy(X[k].copy()).to(dev) for k in range(K)]
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    cloud0 = V.cloud_vector(P, 9)
+    aux0 = V.cloud_vector(P, 10)
+    cloud = torch.from_numpy(cloud0.copy()).to(dev)
+    aux = torch.from_numpy(aux0.copy()).to(dev)
+    step = ops.ServerStep(algo, cloud, lr=0.3, coef=0.6,
+                          aux=None if algo == "fedavg" else aux)
+    ops.reduce_rows_step(rows, w32, step, W=W, mapping=mapping)
+    want = ref.ServerState(algo, cloud0, dict(lr=0.3), coef=0.6,
+                           aux=None if algo == "fedavg" else aux0)
+    want.step(avg)
+    np.testing.assert_array_equal(bits(cloud.cpu().numpy()), bits(want.cloud))
+    if algo != "fedavg":
+        np.testing.assert_array_equal(bits(aux.cpu().numpy()), bits(want.aux))

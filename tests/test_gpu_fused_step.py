@@ -79,11 +79,12 @@ def _check(st, avg, d, algo, opt):
         np.testing.assert_array_equal(bits(d["avg"].cpu().numpy()), bits(avg))
 
 
+@pytest.mark.parametrize("mapping", ["wide", "narrow1", "narrow2"])
 @pytest.mark.parametrize("C", [1024, 2048, 4096])
-@pytest.mark.parametrize("P", [1, 5, 4099, 70_001])
+@pytest.mark.parametrize("P", [1, 5, 4099, 70_001, 70_002])
 @pytest.mark.parametrize("opt", list(OPTS))
 @pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
-def test_reduce_step_bitwise(algo, opt, P, C, dev):
+def test_reduce_step_bitwise(algo, opt, P, C, mapping, dev):
     from fedsim_amd import ops
 
     o = OPTS[opt]
@@ -101,8 +102,9 @@ def test_reduce_step_bitwise(algo, opt, P, C, dev):
     # two ring segments: rows 0..h-1 into an accumulator, the rest fused
     h = K // 3
     acc = torch.empty(P, device=dev)
-    ops.reduce_blocked(Xb, w32[:h].contiguous(), acc, B=h)
-    ops.reduce_blocked_step(Xb, w32[h:].contiguous(), step, B=K - h, acc_in=acc, W=W, r0=h)
+    ops.reduce_blocked(Xb, w32[:h].contiguous(), acc, B=h, flags=ops.tuning_flags(mapping=mapping))
+    ops.reduce_blocked_step(Xb, w32[h:].contiguous(), step, B=K - h, acc_in=acc, W=W, r0=h,
+                            mapping=mapping)
     _check(st, avg, d, algo, o)
 
 

@@ -12,12 +12,19 @@ pytestmark = pytest.mark.gpu
 
 CASES = golden_cases()
 PARAM_CASES = [c for c in CASES if all(c["ok"]) and c["has_params"] and "opts" not in c]
+# "default" lets the library pick the column mapping (narrow at these sizes);
+# the others force the wide f32x4-slot kernels or a narrow (one / two columns
+# per lane) one with a given unroll
 VARIANTS = {
     "default": dict(),
-    "u4v2nt": dict(unroll=4, vpt=2, nt=True),
-    "u8v1": dict(unroll=8, vpt=1),
-    "u16v2": dict(unroll=16, vpt=2),
-    "u4v1nt": dict(unroll=4, vpt=1, nt=True),
+    "u4v2nt": dict(unroll=4, vpt=2, nt=True, mapping="wide"),
+    "u8v1": dict(unroll=8, vpt=1, mapping="wide"),
+    "u16v2": dict(unroll=16, vpt=2, mapping="wide"),
+    "u4v1nt": dict(unroll=4, vpt=1, nt=True, mapping="wide"),
+    "n1u8nt": dict(unroll=8, nt=True, mapping="narrow1"),
+    "n1u32": dict(unroll=32, mapping="narrow1"),
+    "n2u16nt": dict(unroll=16, nt=True, mapping="narrow2"),
+    "n2u8": dict(unroll=8, mapping="narrow2"),
 }
 
 
@@ -60,11 +67,14 @@ def test_reduce_slab_bitwise(case, variant, dev, golden):
     _expect(case, arrays, "avg", out.cpu().numpy())
 
 
+@pytest.mark.parametrize("mapping", ["auto", "wide", "narrow2"])
 @pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
-def test_reduce_rows_and_batches_bitwise(case, dev, golden):
+def test_reduce_rows_and_batches_bitwise(case, mapping, dev, golden):
     """Row-table kernel, and the reduction split into batches chained through
     the accumulator, both equal the single-pass reference result."""
     from fedsim_amd import ops
+
+    fl = ops.tuning_flags(mapping=mapping)
 
     _, arrays = golden
     X = _inputs(case)
@@ -72,7 +82,7 @@ def test_reduce_rows_and_batches_bitwise(case, dev, golden):
     rows = [torch.from_numpy(X[k].copy()).to(dev) for k in idx]
     w32 = torch.tensor([ops.fl32(w) for w in ws], dtype=torch.float32, device=dev)
     out = torch.empty(case["P"], dtype=torch.float32, device=dev)
-    ops.reduce_rows(rows, w32, out, W=W)
+    ops.reduce_rows(rows, w32, out, W=W, flags=fl)
     _expect(case, arrays, "avg", out.cpu().numpy())
     # batches of 1, 2, 3, ... rows, finalize fused into the last batch
     acc = torch.empty_like(out)
@@ -82,7 +92,7 @@ def test_reduce_rows_and_batches_bitwise(case, dev, golden):
         k1 = min(len(rows), k0 + b)
         last = k1 == len(rows)
         ops.reduce_rows(rows[k0:k1], w32[k0:k1].contiguous(), acc,
-                        acc_in=None if first else acc, W=W if last else None)
+                        acc_in=None if first else acc, W=W if last else None, flags=fl)
         first, k0, b = False, k1, b + 1
     _expect(case, arrays, "avg", acc.cpu().numpy())
 
@@ -161,7 +171,7 @@ def test_reduce_blocked_bitwise(case, C, dev, golden):
         ops.pack_row(src, Xb, j + 2)
     w32 = torch.tensor([ops.fl32(w) for w in ws], dtype=torch.float32, device=dev)
     out = torch.empty(P, dtype=torch.float32, device=dev)
-    for variant in ("default", "u4v2nt", "u8v1"):
+    for variant in ("default", "u4v2nt", "u8v1", "n1u8nt", "n2u16nt", "n2u8"):
         fl = ops.tuning_flags(**{k: v for k, v in VARIANTS[variant].items() if k != "vpt"})
         ops.reduce_blocked(Xb, w32, out, B=B, W=W, flags=fl, r0=2)
         _expect(case, arrays, "avg", out.cpu().numpy())
