@@ -239,7 +239,7 @@ def main():
     # the kernel the library launched: the fused step path takes only the
     # mapping bits, the plain reduce all of `flags`
     mapping, unroll = ops.column_mapping(
-        P, ops.tuning_flags(mapping=a.mapping) if fused else flags)
+        P, ops.tuning_flags(mapping=a.mapping) if fused else flags, B=K)
     kernel = ("k_reduce_vec" if mapping == "wide" else
               f"k_reduce_narrow<U={unroll}, VW={mapping[-1]}>")
     traffic = load_pmc(a.pmc_json, K, P, kernel,

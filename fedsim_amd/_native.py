@@ -77,8 +77,8 @@ SIGNATURES = {
     "fedagg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "fedagg_column_mapping": (
         ctypes.c_int,
-        [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
-         ctypes.POINTER(ctypes.c_int)],
+        [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
     ),
     "fedagg_reduce_f32": (
         ctypes.c_int,

@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <initializer_list>
 #include <type_traits>
 
 #include "../../include/fedagg.h"
@@ -60,10 +61,14 @@ constexpr int kWeightTile = 2048;  // FEDAGG_LDSW ablation: weights per LDS tile
 //  * P < 2^20: one column per lane, U = 8.  The f32x4-slot kernels cannot fill
 //    256 CUs there (P = 199,210: 6.1 vs 1.3 TB/s at K = 1000);
 //  * P >= 2^20: two columns per lane, U = 16 (U = 8 from 2^24 on), even with
-//    or ahead of the tuned f32x4 kernels: +1.3 % at 1000 x 25 M, +3.8 % at
-//    1000 x 6.25 M, +5.7 % at 10,000 x 3.125 M (config 4's shard).
+//    or ahead of the tuned f32x4 kernels: +0.5..1.3 % at 1000 x 25 M, +3.8 %
+//    at 1000 x 6.25 M, +3.8..5.7 % at 10,000 x 3.125 M (config 4's shard);
+//  * P >= 2^24 with few rows per launch (B <= 128, e.g. config 5's 100-row
+//    pool passes): four columns per lane, U = 8 (+3 % over two at 100 x 125 M:
+//    a workgroup's fixed costs are spread over few rows there).
 constexpr int64_t kNarrowWideP = int64_t(1) << 20;
 constexpr int64_t kNarrowLongP = int64_t(1) << 24;
+constexpr int64_t kNarrowShortB = 128;
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).
@@ -496,12 +501,18 @@ __device__ __forceinline__ Cols<VW> buf_load_cols(__amdgpu_buffer_rsrc_t r, uint
     o.v[0] = __builtin_bit_cast(
         float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff),
                                                     static_cast<int>(soff), NT ? 2 : 0));
-  } else {
+  } else if constexpr (VW == 2) {
     const f32x2 t = __builtin_bit_cast(
         f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(voff),
                                                     static_cast<int>(soff), NT ? 2 : 0));
     o.v[0] = t.x;
     o.v[1] = t.y;
+  } else {
+    const f32x4 t = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(voff),
+                                                     static_cast<int>(soff), NT ? 2 : 0));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o.v[e] = t[e];
   }
   return o;
 }
@@ -558,11 +569,15 @@ struct NarrowStrided {
     Cols<VW> o;
     if constexpr (VW == 1) {
       o.v[0] = ld1<NT>(p, 0);
-    } else {
+    } else if constexpr (VW == 2) {
       const f32x2* q = reinterpret_cast<const f32x2*>(p);
       const f32x2 t = NT ? __builtin_nontemporal_load(q) : *q;
       o.v[0] = t.x;
       o.v[1] = t.y;
+    } else {
+      const f32x4 t = ld4<NT>(p, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o.v[e] = t[e];
     }
     return o;
   }
@@ -616,7 +631,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_narrow(NR rows, const float* 
     for (int e = 0; e < VW; ++e) a[e] = a[e] / W32;
   }
   if (ok) {
-    if constexpr (VW == 2) {
+    if constexpr (VW == 4) {
+      epi.vec(c0 * 4, f32x4{a[0], a[1], a[2], a[3]});
+    } else if constexpr (VW == 2) {
       epi.vec(c0 * 4, f32x2{a[0], a[1]});
     } else {
       epi.one(c0, a[0]);
@@ -867,20 +884,36 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
                 FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_MAP_MASK))
     return FEDAGG_EINVAL;
+  if (((flags & FEDAGG_MAP_MASK) >> FEDAGG_MAP_SHIFT) > 4) return FEDAGG_EINVAL;
   return 0;
 }
 
 // Columns per lane of the narrow mapping for this call, or 0 for the wide
 // (f32x4-slot) kernels.  `vw_ok` says whether 2 columns per lane are possible
 // (P even, 8-byte aligned operands).
-int narrow_vw(int flags, int64_t P, bool vw2_ok) {
+int narrow_vw(int flags, int64_t P, int64_t B, int max_vw) {
   const int m = (flags & FEDAGG_MAP_MASK) >> FEDAGG_MAP_SHIFT;
   int vw;
   if (m == 1) return 0;
   if (m == 2) vw = 1;
   else if (m == 3) vw = 2;
-  else vw = P < kNarrowWideP ? 1 : 2;
-  return (vw == 2 && !vw2_ok) ? 1 : vw;
+  else if (m == 4) vw = 4;
+  else if (P < kNarrowWideP) vw = 1;
+  else vw = (P >= kNarrowLongP && B <= kNarrowShortB) ? 4 : 2;
+  while (vw > max_vw) vw /= 2;
+  return vw;
+}
+
+// The widest columns-per-lane (1 / 2 / 4) that P and the operands' alignment
+// allow.
+int max_cols_per_lane(int64_t P, std::initializer_list<const void*> ptrs) {
+  int v = (P % 4 == 0) ? 4 : (P % 2 == 0) ? 2 : 1;
+  for (const void* q : ptrs) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(q);
+    if (v == 4 && (a & 15u)) v = 2;
+    if (v == 2 && (a & 7u)) v = 1;
+  }
+  return v;
 }
 
 template <int U, int VW, bool NT, class NR, class Epi>
@@ -922,6 +955,9 @@ hipError_t launch_narrow_store(const NR& rows, int vw, const float* w, int64_t B
                                hipStream_t s) {
   const EpiStore st{out};
   const bool nt = (flags & FEDAGG_NT) != 0;
+  if (vw == 4)
+    return nt ? launch_narrow_u<4, true>(rows, w, B, P, acc_in, st, W32, flags, s)
+              : launch_narrow_u<4, false>(rows, w, B, P, acc_in, st, W32, flags, s);
   if (vw == 2)
     return nt ? launch_narrow_u<2, true>(rows, w, B, P, acc_in, st, W32, flags, s)
               : launch_narrow_u<2, false>(rows, w, B, P, acc_in, st, W32, flags, s);
@@ -934,11 +970,11 @@ template <class NR, class Epi>
 hipError_t launch_narrow_step(const NR& rows, int vw, const float* w, int64_t B, int64_t P,
                               const float* acc_in, const Epi& epi, float W32, int flags,
                               hipStream_t s) {
+  if (vw == 4) return launch_narrow_u<4, true>(rows, w, B, P, acc_in, epi, W32, flags, s);
   return vw == 2 ? launch_narrow_u<2, true>(rows, w, B, P, acc_in, epi, W32, flags, s)
                  : launch_narrow_u<1, true>(rows, w, B, P, acc_in, epi, W32, flags, s);
 }
 
-inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 
 // Column-block widths the blocked kernels are built for (one workgroup's span
 // of the wide mapping; a multiple of the narrow mapping's 256 * 2 columns).
@@ -994,9 +1030,10 @@ extern "C" {
 
 int fedagg_abi_version(void) { return FEDAGG_ABI_VERSION; }
 
-int fedagg_column_mapping(int64_t P, int flags, int vw2_ok, int* vw, int* unroll) {
-  if (P < 0 || !vw || !unroll) return FEDAGG_EINVAL;
-  *vw = narrow_vw(flags, P, vw2_ok != 0);
+int fedagg_column_mapping(int64_t P, int64_t B, int flags, int max_vw, int* vw, int* unroll) {
+  if (P < 0 || B < 0 || !vw || !unroll || (max_vw != 1 && max_vw != 2 && max_vw != 4))
+    return FEDAGG_EINVAL;
+  *vw = narrow_vw(flags, P, B, max_vw);
   *unroll = *vw ? narrow_unroll(flags, P) : 0;
   return 0;
 }
@@ -1017,11 +1054,14 @@ int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B, in
   const bool init = (flags & FEDAGG_INIT) != 0;
   const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(X) && (ldx % 4 == 0) &&
                       aligned16(out) && (init || aligned16(acc_in));
-  const bool vw2_ok = !(flags & FEDAGG_SCALAR) && P % 2 == 0 && aligned8(X) && ldx % 2 == 0 &&
-                      aligned8(out) && (init || aligned8(acc_in));
+  // row k starts at X + k*ldx: ldx's alignment counts like a pointer's
+  const int max_vw = (flags & FEDAGG_SCALAR)
+                         ? 1
+                         : max_cols_per_lane(P, {X, reinterpret_cast<const void*>(ldx * 4), out,
+                                                 init ? nullptr : acc_in});
   hipStream_t s = static_cast<hipStream_t>(stream);
   // misaligned rows take the one-column-per-lane kernel whatever the mapping
-  const int vw = vec_ok ? narrow_vw(flags, P, vw2_ok) : 1;
+  const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
   if (vw) return static_cast<int>(launch_narrow_store(NarrowStrided{X, ldx}, vw, w, B, P, acc_in,
                                                       out, W32, flags, s));
   return static_cast<int>(dispatch_reduce(RowsStrided{X, ldx}, w, B, P, acc_in, out, W32, flags, s));
@@ -1037,10 +1077,12 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
   // sync: the caller passes FEDAGG_SCALAR unless every rows[k] is 16-B aligned.
   const bool init = (flags & FEDAGG_INIT) != 0;
   const bool vec_ok = !(flags & FEDAGG_SCALAR) && aligned16(out) && (init || aligned16(acc_in));
-  // 16-B aligned rows (no FEDAGG_SCALAR) are 8-B aligned too
-  const bool vw2_ok = vec_ok && P % 2 == 0;
+  // without FEDAGG_SCALAR the caller promises 16-B aligned rows
+  const int max_vw = (flags & FEDAGG_SCALAR)
+                         ? 1
+                         : max_cols_per_lane(P, {out, init ? nullptr : acc_in});
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int vw = vec_ok ? narrow_vw(flags, P, vw2_ok) : 1;
+  const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
   if (vw)
     return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B, P,
                                                 acc_in, out, W32, flags, s));
@@ -1067,7 +1109,9 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   const bool region32 = Kcap * C * 4 < (int64_t(1) << 32);
   const int vw = (flags & (FEDAGG_LDSW | FEDAGG_FLAT)) || !region32
                      ? 0
-                     : narrow_vw(flags, P, P % 2 == 0 && ((flags & FEDAGG_INIT) || aligned8(acc_in)));
+                     : narrow_vw(flags, P, B,
+                                 max_cols_per_lane(P, {out, (flags & FEDAGG_INIT) ? nullptr
+                                                                                 : acc_in}));
   // buffer-descriptor path unless asked for flat loads or a block region is
   // too large for a 32-bit descriptor range
   if (vw) {
@@ -1201,7 +1245,7 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
     return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const RowsBlockedBuf rows{Xb, Kcap, C};
-  const int vw = narrow_vw(flags, P, P % 2 == 0);
+  const int vw = narrow_vw(flags, P, B, max_cols_per_lane(P, {}));  // operands 16-B aligned
   // the per-C default configuration of fedagg_reduce_blocked_f32 (256 lanes,
   // VPT = C/1024, U = 4 at C=4096 else 2, non-temporal loads), or the narrow
   // mapping at small P
@@ -1243,7 +1287,7 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   // per lane, U = kRowsUnroll); the rows are the caller's separate
   // allocations, read through buffer descriptors unless FEDAGG_FLAT
   const bool nt = (flags & FEDAGG_NT) != 0;
-  const int vw = narrow_vw(flags, P, P % 2 == 0);
+  const int vw = narrow_vw(flags, P, B, max_cols_per_lane(P, {}));  // operands 16-B aligned
   if (vw) {
     const NarrowTable tab{rows, table_row_bytes(P)};
     hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {

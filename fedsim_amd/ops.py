@@ -45,10 +45,11 @@ def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
     (row-major / pointer-table layouts), non-temporal loads, the workgroup
     size of the column-blocked layout, flat (instead of buffer-descriptor)
     loads for it, and the column mapping (``"auto"``, ``"wide"`` = f32x4
-    slots, ``"narrow1"`` / ``"narrow2"`` = one / two columns per lane).
+    slots, ``"narrow1"`` / ``"narrow2"`` / ``"narrow4"`` = one / two / four
+    columns per lane).
     0 / False / "auto" = library default."""
     sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4, 32: 5}[unroll]
-    msel = {"auto": 0, "wide": 1, "narrow1": 2, "narrow2": 3}[mapping]
+    msel = {"auto": 0, "wide": 1, "narrow1": 2, "narrow2": 3, "narrow4": 4}[mapping]
     vsel = {0: 0, 1: 1, 2: 2, 4: 3}[vpt]
     bsel = {0: 0, 256: 1, 512: 2, 1024: 3}[bs]
     return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
@@ -66,12 +67,14 @@ _FLAGS_BY_C = {4096: tuning_flags(unroll=4, nt=True), 2048: tuning_flags(unroll=
 _MIN_WORKGROUPS = 2048  # ~8 per CU: below this, narrower column blocks win
 
 
-def column_mapping(P: int, flags: int = 0, vw2_ok: bool = True):
-    """The reduce kernel the library picks for P columns under ``flags``
+def column_mapping(P: int, flags: int = 0, max_vw: int = 4, B: int = 1000):
+    """The reduce kernel the library picks for B rows x P columns under ``flags``
     (fedagg_column_mapping): ``("wide", None)`` for the f32x4-slot kernels,
-    else ``("narrow<vw>", unroll)``."""
+    else ``("narrow<vw>", unroll)``.  ``max_vw``: the most columns per lane
+    the operands' alignment allows (P's divisibility is applied here)."""
     vw, u = ctypes.c_int(), ctypes.c_int()
-    check(_native.load().fedagg_column_mapping(P, flags, int(vw2_ok), ctypes.byref(vw),
+    max_vw = min(max_vw, 4 if P % 4 == 0 else 2 if P % 2 == 0 else 1)
+    check(_native.load().fedagg_column_mapping(P, B, flags, max_vw, ctypes.byref(vw),
                                                 ctypes.byref(u)), "fedagg_column_mapping")
     return ("wide", None) if vw.value == 0 else (f"narrow{vw.value}", u.value)
 

@@ -81,15 +81,17 @@ extern "C" {
 /* ablation: stage the per-client weights through LDS tiles instead of reading
  * them with wave-uniform scalar loads (same results; A/B measurement switch) */
 #define FEDAGG_LDSW     0x20000
-/* bits 18..19: column mapping of the reduce kernels.  An in-order per-column
+/* bits 18..20: column mapping of the reduce kernels.  An in-order per-column
  * sum is parallel over columns only, so at small P the f32x4-slot ("wide")
  * kernels leave CUs idle (P = 199,210 is 778 waves).  0 = library default
- * (narrow: one column per lane below P = 2^20, two from there on), 1 = wide
- * (f32x4 slots; the unroll / VPT / BS tuning bits apply to it), 2 = narrow,
- * one column per lane, 3 = narrow, two columns per lane (falls back to one
- * when P is odd or an operand is not 8-byte aligned).  Same results. */
+ * (narrow: one column per lane below P = 2^20, two from there on, four for
+ * P >= 2^24 with at most 128 rows per call), 1 = wide
+ * (f32x4 slots; the unroll / VPT / BS tuning bits apply to it), 2 / 3 / 4 =
+ * narrow with one / two / four columns per lane (each workgroup 256 lanes;
+ * falls back to fewer columns when P or an operand's alignment does not
+ * allow them).  Same results. */
 #define FEDAGG_MAP_SHIFT 18
-#define FEDAGG_MAP_MASK  0xC0000
+#define FEDAGG_MAP_MASK  0x1C0000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
@@ -102,13 +104,13 @@ int fedagg_abi_version(void);
 const char* fedagg_strerror(int code);
 
 /*
- * Which reduce kernel a call with these flags takes for P columns (host-side
- * decision, no device access): *vw = columns per lane of the narrow mapping
- * (1 or 2), or 0 for the wide f32x4-slot kernels; *unroll = the narrow
- * kernel's k-unroll (0 when wide).  vw2_ok: whether two columns per lane are
- * possible (P even, operands 8-byte aligned).
+ * Which reduce kernel a call with these flags takes for B rows x P columns
+ * (host-side decision, no device access): *vw = columns per lane of the
+ * narrow mapping (1, 2 or 4), or 0 for the wide f32x4-slot kernels; *unroll =
+ * the narrow kernel's k-unroll (0 when wide).  max_vw (1, 2 or 4): the most
+ * columns per lane P and the operands' alignment allow.
  */
-int fedagg_column_mapping(int64_t P, int flags, int vw2_ok, int* vw, int* unroll);
+int fedagg_column_mapping(int64_t P, int64_t B, int flags, int max_vw, int* vw, int* unroll);
 
 /*
  * Weighted sequential reduction of B client rows into one accumulator.

@@ -86,7 +86,7 @@ def test_argument_validation_without_device(lib):
     assert lib.fedagg_reduce_f32(null, 4, 16, 1, 4, null, 16, 1.0, 1, null) == E
     assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 0, null) == E  # no INIT, no acc
     assert lib.fedagg_reduce_f32(16, 2, 16, 1, 4, null, 16, 1.0, 1, null) == E  # ldx < P
-    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 1 | 0x100000, null) == E
+    assert lib.fedagg_reduce_f32(16, 4, 16, 1, 4, null, 16, 1.0, 1 | 0x800000, null) == E
     assert lib.fedagg_reduce_f32(16, 1 << 31, 16, 1, (1 << 30) + 1, null, 16, 1.0, 1, null) == E
     assert lib.fedagg_reduce_rows_f32(null, 16, 1, 4, null, 16, 1.0, 1, null) == E
     assert lib.fedagg_finalize_f32(null, 1.0, 4, 16, null) == E
@@ -162,9 +162,16 @@ def test_column_mapping_decision():
     assert ops.column_mapping(199_210) == ("narrow1", 8)
     assert ops.column_mapping(1_085_668) == ("narrow2", 16)
     assert ops.column_mapping(25_000_000) == ("narrow2", 8)
-    assert ops.column_mapping(25_000_000, vw2_ok=False) == ("narrow1", 8)
+    assert ops.column_mapping(125_000_000, B=100) == ("narrow4", 8)  # short pool passes
+    assert ops.column_mapping(125_000_000, B=129) == ("narrow2", 8)
+    assert ops.column_mapping(1_085_668, B=100) == ("narrow2", 16)
+    assert ops.column_mapping(25_000_000, max_vw=1) == ("narrow1", 8)
+    assert ops.column_mapping(25_000_001) == ("narrow1", 8)  # odd P: one column per lane
+    assert ops.column_mapping(8, ops.tuning_flags(mapping="narrow4")) == ("narrow4", 8)
+    assert ops.column_mapping(6, ops.tuning_flags(mapping="narrow4")) == ("narrow2", 8)
     assert ops.column_mapping(25_000_000, ops.tuning_flags(mapping="wide")) == ("wide", None)
-    assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow2", unroll=32)) == ("narrow2", 32)
+    assert ops.column_mapping(8, ops.tuning_flags(mapping="narrow2", unroll=32)) == ("narrow2", 32)
+    assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow2", unroll=32)) == ("narrow1", 32)
     assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow1", unroll=16)) == ("narrow1", 16)
     # unroll selectors the narrow kernels do not build fall back to the default
     assert ops.column_mapping(199_210, ops.tuning_flags(unroll=4)) == ("narrow1", 8)

@@ -186,8 +186,8 @@ def test_borrowed_full_size_round(dev):
     np.testing.assert_array_equal(bits(cloud.index_select(0, cols).cpu().numpy()), bits(exp_cloud))
 
 
-@pytest.mark.parametrize("P", [5, 70_001, 70_002])
-@pytest.mark.parametrize("mapping", ["wide", "narrow1", "narrow2"])
+@pytest.mark.parametrize("P", [5, 70_001, 70_002, 70_004])
+@pytest.mark.parametrize("mapping", ["wide", "narrow1", "narrow2", "narrow4"])
 @pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
 def test_rows_step_mappings_bitwise(algo, mapping, P, dev):
     """fedagg_reduce_step_rows_f32 under each column mapping (two columns per

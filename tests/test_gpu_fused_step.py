@@ -79,9 +79,9 @@ def _check(st, avg, d, algo, opt):
         np.testing.assert_array_equal(bits(d["avg"].cpu().numpy()), bits(avg))
 
 
-@pytest.mark.parametrize("mapping", ["wide", "narrow1", "narrow2"])
+@pytest.mark.parametrize("mapping", ["wide", "narrow1", "narrow2", "narrow4"])
 @pytest.mark.parametrize("C", [1024, 2048, 4096])
-@pytest.mark.parametrize("P", [1, 5, 4099, 70_001, 70_002])
+@pytest.mark.parametrize("P", [1, 5, 4099, 70_001, 70_002, 70_004])
 @pytest.mark.parametrize("opt", list(OPTS))
 @pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
 def test_reduce_step_bitwise(algo, opt, P, C, mapping, dev):

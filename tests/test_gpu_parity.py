@@ -25,6 +25,8 @@ VARIANTS = {
     "n1u32": dict(unroll=32, mapping="narrow1"),
     "n2u16nt": dict(unroll=16, nt=True, mapping="narrow2"),
     "n2u8": dict(unroll=8, mapping="narrow2"),
+    "n4u8nt": dict(unroll=8, nt=True, mapping="narrow4"),
+    "n4u32": dict(unroll=32, mapping="narrow4"),
 }
 
 
@@ -67,7 +69,7 @@ def test_reduce_slab_bitwise(case, variant, dev, golden):
     _expect(case, arrays, "avg", out.cpu().numpy())
 
 
-@pytest.mark.parametrize("mapping", ["auto", "wide", "narrow2"])
+@pytest.mark.parametrize("mapping", ["auto", "wide", "narrow2", "narrow4"])
 @pytest.mark.parametrize("case", PARAM_CASES, ids=[c["id"] for c in PARAM_CASES])
 def test_reduce_rows_and_batches_bitwise(case, mapping, dev, golden):
     """Row-table kernel, and the reduction split into batches chained through
@@ -171,7 +173,7 @@ def test_reduce_blocked_bitwise(case, C, dev, golden):
         ops.pack_row(src, Xb, j + 2)
     w32 = torch.tensor([ops.fl32(w) for w in ws], dtype=torch.float32, device=dev)
     out = torch.empty(P, dtype=torch.float32, device=dev)
-    for variant in ("default", "u4v2nt", "u8v1", "n1u8nt", "n2u16nt", "n2u8"):
+    for variant in ("default", "u4v2nt", "u8v1", "n1u8nt", "n2u16nt", "n2u8", "n4u8nt"):
         fl = ops.tuning_flags(**{k: v for k, v in VARIANTS[variant].items() if k != "vpt"})
         ops.reduce_blocked(Xb, w32, out, B=B, W=W, flags=fl, r0=2)
         _expect(case, arrays, "avg", out.cpu().numpy())

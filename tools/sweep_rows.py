@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedsim_amd import ops  # noqa: E402
 
 SHAPES = ((2, 4), (4, 2), (4, 4), (8, 1), (8, 2), (8, 4), (16, 1), (16, 2), (4, 1))
+NARROW = (("narrow1", 8), ("narrow1", 16), ("narrow2", 8), ("narrow2", 16), ("narrow4", 8))
 
 
 def main():
@@ -38,21 +39,24 @@ def main():
     w32 = torch.randint(50, 601, (K,), device=dev).float()
     out = torch.empty(P, device=dev)
     ref = torch.empty(P, device=dev)
-    ops.reduce_rows(rows, w32, ref, W=1.0, flags=ops.tuning_flags(unroll=4, vpt=2, flat=True),
+    ops.reduce_rows(rows, w32, ref, W=1.0,
+                    flags=ops.tuning_flags(unroll=4, vpt=2, flat=True, mapping="wide"),
                     table=table)
     cloud0 = torch.empty(P, device=dev).normal_(0, 0.05, generator=g)
     cloud = cloud0.clone()
     cloud_ref = None
 
-    variants = [dict(kind="reduce", unroll=u, vpt=v, flat=f)
+    variants = [dict(kind="reduce", unroll=u, vpt=v, flat=f, mapping="wide")
                 for f in (False, True) for u, v in SHAPES]
-    variants += [dict(kind="step", flat=f) for f in (False, True)]
+    variants += [dict(kind="reduce", unroll=u, mapping=m, flat=False) for m, u in NARROW]
+    variants += [dict(kind="step", flat=f, mapping="wide") for f in (False, True)]
+    variants += [dict(kind="step", flat=False, mapping="auto")]
     times = {i: [] for i in range(len(variants))}
     for r in range(a.rounds):
         for i, var in enumerate(variants):
             if var["kind"] == "reduce":
-                fl = ops.tuning_flags(unroll=var["unroll"], vpt=var["vpt"], nt=True,
-                                      flat=var["flat"])
+                fl = ops.tuning_flags(unroll=var["unroll"], vpt=var.get("vpt", 0), nt=True,
+                                      flat=var["flat"], mapping=var["mapping"])
 
                 def run():
                     ops.reduce_rows(rows, w32, out, W=1.0, flags=fl, table=table)
@@ -61,7 +65,8 @@ def main():
 
                 def run():
                     cloud.copy_(cloud0)  # timed separately below; same in every variant
-                    ops.reduce_rows_step(rows, w32, step, W=1.0, table=table, flat=var["flat"])
+                    ops.reduce_rows_step(rows, w32, step, W=1.0, table=table, flat=var["flat"],
+                                         mapping=var["mapping"])
 
             run()
             torch.cuda.synchronize()
