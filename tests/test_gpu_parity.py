@@ -209,3 +209,50 @@ def test_pack_row_layout(dev):
             for k in range(K):
                 ops.pack_row(Xu[k, 1:], Xb3, k)  # 4-byte aligned source
             assert torch.equal(Xb3, ref_b)
+
+
+@pytest.mark.parametrize("mapping", ["auto", "wide", "narrow1", "narrow2", "narrow4"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8, 9, 255, 256, 257, 1022, 1025])
+def test_mappings_small_and_ragged_P(P, mapping, dev):
+    """Every column mapping at sizes around its per-lane width and workgroup
+    span (the two- and four-column kernels fall back when P does not divide),
+    with acc_in chaining, against the oracle."""
+    from fedsim_amd import ops
+
+    K = 7
+    X = V.client_rows("normal", K, P, 31 + P)
+    w = V.client_weights("fedavg", K, 31 + P)
+    Xd = torch.from_numpy(X).to(dev)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    fl = ops.tuning_flags(mapping=mapping)
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    ops.reduce_slab(Xd[:3], w32[:3], out, flags=fl)
+    ops.reduce_slab(Xd[3:], w32[3:].contiguous(), out, acc_in=out, W=sum(w), flags=fl)
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref.reduce(X, w, W=sum(w))))
+
+
+@pytest.mark.parametrize("mapping", ["narrow2", "narrow4"])
+def test_mappings_misaligned_operands(mapping, dev):
+    """Rows, accumulator and output at 4- and 8-byte offsets: the wider narrow
+    kernels step down to what the alignment allows; same bits."""
+    from fedsim_amd import ops
+
+    K, P = 6, 4100
+    X = V.client_rows("realistic", K, P + 2, 5)
+    w = V.client_weights("fedavg", K, 5)
+    W = sum(w)
+    big = torch.from_numpy(X).to(dev)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    fl = ops.tuning_flags(mapping=mapping)
+    for off in (1, 2):
+        rows = big[:, off:off + P]
+        want = ref.reduce(np.ascontiguousarray(X[:, off:off + P]), w, W=W)
+        buf = torch.empty(P + 4, dtype=torch.float32, device=dev)
+        out = buf[off:off + P]
+        ops.reduce_slab(rows[:2], w32[:2], out, flags=fl)
+        ops.reduce_slab(rows[2:], w32[2:].contiguous(), out, acc_in=out, W=W, flags=fl)
+        np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(want))
+        tab_rows = [rows[k] for k in range(K)]
+        out2 = torch.empty(P, dtype=torch.float32, device=dev)
+        ops.reduce_rows(tab_rows, w32, out2, W=W, flags=fl)
+        np.testing.assert_array_equal(bits(out2.cpu().numpy()), bits(want))
