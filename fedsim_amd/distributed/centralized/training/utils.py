@@ -38,7 +38,9 @@ def serial_aggregation(
     other_weight=None,
     purge_msg=True,
 ):
-    params = client_msg["local_params"].detach()
+    params = client_msg["local_params"]
+    if params.requires_grad:  # detach only when needed: it allocates a tensor object
+        params = params.detach()
     diverged = client_msg["diverged"]
     metrics = client_msg["metrics"]
     n_samples = client_msg["num_samples"]

@@ -163,16 +163,19 @@ def reduce_rows(
     W: Optional[float] = None,
     flags: int = 0,
     table: Optional[torch.Tensor] = None,
+    checked: bool = False,
 ) -> torch.Tensor:
     """Same as :func:`reduce_slab` but each client row is its own HIP tensor
     (no packing copy).  ``table`` may pass a pre-filled int64 device tensor of
-    row pointers; otherwise one is built and uploaded."""
+    row pointers; otherwise one is built and uploaded.  ``checked``: every row
+    is known to be a contiguous, 16-B aligned fp32 HIP tensor of P elements
+    (skip the per-row checks)."""
     _require_hip_f32(out, "out")
     _require_hip_f32(w32, "w32")
     P = out.numel()
     B = len(rows)
     aligned = True
-    for i, r in enumerate(rows):
+    for i, r in enumerate(() if checked else rows):
         _require_hip_f32(r, f"rows[{i}]")
         if r.numel() != P or not r.is_contiguous():
             raise ValueError(f"rows[{i}] must be contiguous with {P} elements")
@@ -480,16 +483,19 @@ def reduce_rows_step(
     flat: bool = False,
     mapping: str = "auto",
     unroll: int = 0,
+    checked: bool = False,
 ) -> torch.Tensor:
     """reduce_rows(rows, ..., out=avg) then step.apply(avg), fused into one
     pass over the caller's own client tensors (fedagg_reduce_step_rows_f32):
     the zero-copy round of HBM-resident client vectors.  Returns step.cloud.
     ``flat`` selects 64-bit flat loads instead of per-row buffer descriptors
-    (ablation; same arithmetic)."""
+    (ablation; same arithmetic).  ``checked``: the caller has already
+    validated every row (the aggregator does at ``add``), skip the per-row
+    checks."""
     _require_hip_f32(w32, "w32")
     P, dev = step.P, step.cloud.device
     B = len(rows)
-    for i, r in enumerate(rows):
+    for i, r in enumerate(() if checked else rows):
         _require_hip_f32(r, f"rows[{i}]")
         if r.numel() != P or not r.is_contiguous() or r.data_ptr() % 16:
             raise ValueError(f"rows[{i}] must be contiguous, 16-B aligned, {P} elements")

@@ -29,10 +29,10 @@ fallback for them — without a HIP device / libfedagg the add raises.
 from __future__ import annotations
 
 import os
+import struct
 from collections import deque
 from typing import Dict, List, Optional
 
-import numpy as np
 import torch
 
 from .. import ops
@@ -54,6 +54,13 @@ def _slab_budget(dev: torch.device, requested: Optional[int]) -> int:
     total = torch.cuda.get_device_properties(dev).total_memory
     return min(_SLAB_CAP, total // 4)
 _DEFAULT_MAX_ROWS = int(os.environ.get("FEDSIM_AMD_MAX_ROWS", 4096))
+_F32 = struct.Struct("f")
+
+
+def _fl32(x) -> float:
+    """fl32(x) as a Python float: ATen's rounding of a Python scalar weight
+    (round to nearest even), the same as float(np.float32(x))."""
+    return _F32.unpack(_F32.pack(x))[0]
 _STAGING_SLOTS = 3
 
 
@@ -190,14 +197,19 @@ class _DeviceEntry(object):
     # -- reference semantics -------------------------------------------------
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
-        if tuple(value.shape) != self.shape:
+        if value.shape != self.shape:
             raise ValueError(
                 f"tensor of shape {tuple(value.shape)} added to a key aggregating {self.shape}"
             )
         if value.dtype != torch.float32:
             raise TypeError(f"device aggregation supports float32 tensors, got {value.dtype}")
-        w32 = float(np.float32(weight))
-        src = value.detach().reshape(-1)
+        w32 = _fl32(weight)
+        # the common case (a detached flat vector from vectorize_module) is
+        # taken as is: detach / reshape allocate a new tensor object each,
+        # a few us per client on the host
+        src = value.detach() if value.requires_grad else value
+        if src.dim() != 1:
+            src = src.reshape(-1)
         if self.borrow and self._borrowable(src):
             if self.n_pending:
                 self._flush(final_W=None)  # earlier slab rows first: arrival order
@@ -242,14 +254,16 @@ class _DeviceEntry(object):
         w32 = torch.tensor(self.pending_w, dtype=torch.float32).pin_memory()
         w32 = w32.to(self.dev, non_blocking=True)
         table = ops.row_table(rows, self.dev)
+        # every row passed _borrowable at add: skip the per-row checks
         if step is not None:
-            ops.reduce_rows_step(rows, w32, step, acc_in=self.acc, W=final_W, table=table)
+            ops.reduce_rows_step(rows, w32, step, acc_in=self.acc, W=final_W, table=table,
+                                 checked=True)
         else:
             acc_in = self.acc
             if self.acc is None:
                 self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
             ops.reduce_rows(rows, w32, self.acc, acc_in=acc_in, W=final_W,
-                            flags=ops.FEDAGG_NT, table=table)
+                            flags=ops.FEDAGG_NT, table=table, checked=True)
         for t in rows:  # the caller's allocations may belong to another stream
             t.record_stream(cur)
         self.borrowed = []

@@ -314,3 +314,18 @@ def test_vectorize_module_grads_and_misc_helpers():
 
     assert get_from_module("fedsim_amd.utils", "Storage").__name__ == "Storage"
     assert get_from_module("fedsim_amd.utils", "nope") is None
+
+
+def test_weight_rounding_matches_aten():
+    """The aggregator's fl32(weight) (struct round trip) equals numpy's / ATen's
+    round-to-nearest-even for the weight types serial_aggregation passes."""
+    import numpy as np
+    import torch
+
+    from fedsim_amd.utils.aggregators import _fl32
+
+    vals = [0, 1, 437, 2**24 + 1, 2**25 + 3, 0.1, 1 / 3, -2.5, 1e-45, 3.4e38, 5e-324,
+            np.int64(600), np.float64(0.7), torch.tensor(123.456, dtype=torch.float64), True]
+    for v in vals:
+        assert _fl32(v) == float(np.float32(float(v))), v
+        assert _fl32(v) == float(torch.tensor(float(v), dtype=torch.float32)), v
