@@ -12,24 +12,31 @@
 //
 // Design (MI355X-first, not a translation — the reference has no kernels):
 //   * The reduction is HBM-bound (0.5 flop/byte, no MFMA).  Every client row is
-//     streamed exactly once: each lane owns VPT f32x4 column slots and walks
-//     the K client rows in arrival order, so each wave-instruction reads a
-//     contiguous 1 KiB run of a row and the running sum never leaves VGPRs.
+//     streamed exactly once: each lane owns a few columns and walks the K
+//     client rows in arrival order; the running sum never leaves VGPRs.
+//   * Columns are the only parallelism an in-order sum has, so how many a lane
+//     owns decides whether the chip fills: the default "narrow" kernels
+//     (k_reduce_narrow) give each lane 1, 2 or 4 adjacent columns (256 B, 512 B
+//     or 1 KiB per wave-instruction), the "wide" ones (k_reduce_vec) VPT f32x4
+//     slots.  The library picks per call (fedagg_column_mapping); see
+//     DESIGN.md §3 for the measurements behind the choice.
 //   * Exact mode keeps the reference's per-column order k = 0..K-1 and its
 //     rounding (separate mul and add, no contraction, IEEE true division), so
 //     outputs are bit-identical to the reference CPU aggregation.
 //   * The per-client weight is wave-uniform: it is read with scalar loads
 //     (s_load through the scalar cache, broadcast from SGPRs) — the CDNA way to
 //     broadcast a uniform value, cheaper than an LDS round trip.
-//   * k is unrolled U-deep: U*VPT independent 16-byte loads are issued before
-//     the in-order adds consume them, so each wave keeps U*VPT KiB in flight.
+//   * k is unrolled U-deep: U rows of independent loads are issued before the
+//     in-order adds consume them (the last B mod U rows too, under
+//     wave-uniform guards), so every wave keeps several KiB in flight.
 //   * HBM layout: the aggregator packs client rows into a COLUMN-BLOCKED slab
-//     (one workgroup's column span holds all K rows contiguously), so each
-//     workgroup streams one contiguous region.  Those loads go through one
-//     buffer descriptor per workgroup with the row in an SGPR soffset:
-//     buffer_load_dwordx4 v, v_off, s[rsrc], s_row offen nt.
-//   * Layout / unroll / lanes-per-slot / nt were chosen by measurement
-//     (tools/sweep_reduce.py, profiles/r01_sweep*/).
+//     (a column block holds all K rows of its C columns contiguously), so each
+//     block's workgroups stream one contiguous region.  Those loads go through
+//     one buffer descriptor per workgroup with the row in an SGPR soffset:
+//     buffer_load_dword{,x2,x4} v, v_off, s[rsrc], s_row offen nt.
+//   * Layout / mapping / unroll / nt were chosen by measurement
+//     (tools/sweep_reduce.py, tools/sweep_mapping.py, tools/ab_mapping.py,
+//     profiles/).
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
 // (see __graft_entry__.build()).
