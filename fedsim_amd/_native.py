@@ -34,6 +34,7 @@ FEDAGG_BS_SHIFT = 14
 FEDAGG_FLAT = 0x10000
 FEDAGG_LDSW = 0x20000
 FEDAGG_MAP_SHIFT = 18
+FEDAGG_FAST = 0x200000
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0

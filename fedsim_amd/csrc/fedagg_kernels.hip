@@ -535,9 +535,10 @@ struct NarrowBlocked {
   __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
     return static_cast<uint32_t>(c & (C - 1)) * 4u;
   }
-  template <int VW, bool NT>
+  // SPAN: columns one workgroup covers (all inside one block)
+  template <int VW, bool NT, int SPAN = kBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
-    const int64_t b = (static_cast<int64_t>(blockIdx.x) * kBlock * VW) >> __builtin_ctzll(C);
+    const int64_t b = (static_cast<int64_t>(blockIdx.x) * SPAN) >> __builtin_ctzll(C);
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(X + b * Kcap * C), static_cast<short>(0),
         static_cast<int>(static_cast<uint32_t>(Kcap * C * 4)), 0x00020000);
@@ -553,7 +554,7 @@ struct NarrowTable {
   __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
     return static_cast<uint32_t>(c) * 4u;
   }
-  template <int VW, bool NT>
+  template <int VW, bool NT, int SPAN = kBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(rows[k]), static_cast<short>(0), static_cast<int>(row_bytes),
@@ -570,7 +571,7 @@ struct NarrowStrided {
   __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
     return static_cast<uint32_t>(c) * 4u;
   }
-  template <int VW, bool NT>
+  template <int VW, bool NT, int SPAN = kBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
     const char* p = reinterpret_cast<const char*>(X + k * ldx) + voff;
     Cols<VW> o;
@@ -645,6 +646,73 @@ __global__ __launch_bounds__(kBlock) void k_reduce_narrow(NR rows, const float* 
     } else {
       epi.one(c0, a[0]);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fast (reordered) mode, FEDAGG_FAST: split-K for few columns and many rows.
+// Below ~64 columns per SIMD even one column per lane cannot fill the chip
+// (a 7,850-parameter logistic regression is 123 waves), so the K rows of a
+// 64-column tile are split over the S waves of a workgroup:
+//   * wave s takes rows k0 + s*U .. k0 + s*U + U-1 of every S*U-row step;
+//     lane l owns column tile*64 + l (256 B per wave-instruction);
+//   * the per-client weights of a 4096-row tile are staged once in LDS by the
+//     whole workgroup and read back as wave-uniform (broadcast) ds_reads;
+//   * each wave keeps a running fmaf partial sum; the S partials are combined
+//     through LDS by wave 0 in a fixed order (s = 0..S-1, then acc_in), so the
+//     result is deterministic run to run but NOT the reference's summation
+//     order: parity is normwise, like the client-sharded
+//     all-reduce.
+// ---------------------------------------------------------------------------
+constexpr int kSplitWeights = 4096;
+
+template <int S, int U, bool NT, class NR, class Epi>
+__global__ __launch_bounds__(64 * S) void k_reduce_splitk(NR rows, const float* __restrict__ w,
+                                                          int64_t B, int64_t P,
+                                                          const float* acc_in, Epi epi,
+                                                          float W32, int flags) {
+  __shared__ float wsh[kSplitWeights];
+  __shared__ float part[S][64];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const bool ok = c0 < P;
+  const int64_t c = ok ? c0 : P - 1;
+  const uint32_t voff = rows.template lane_off<1>(c);
+  float a = 0.f;
+  for (int64_t t0 = 0; t0 < B; t0 += kSplitWeights) {
+    const int64_t n = (B - t0) < kSplitWeights ? (B - t0) : kSplitWeights;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < n; i += 64 * S) wsh[i] = w[t0 + i];
+    __syncthreads();
+    int64_t k = wv * U;  // tile-relative row of this wave's first load
+    for (; k + U <= n; k += S * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = rows.template load<1, NT, 64>(t0 + k + u, voff).v[0];
+#pragma unroll
+      for (int u = 0; u < U; ++u) a = __builtin_fmaf(v[u], wsh[k + u], a);
+    }
+    if (k < n) {  // this wave's last, partial step of the tile
+      const int64_t rem = n - k;
+      float v[U - 1];
+#pragma unroll
+      for (int u = 0; u < U - 1; ++u)
+        if (u < rem) v[u] = rows.template load<1, NT, 64>(t0 + k + u, voff).v[0];
+#pragma unroll
+      for (int u = 0; u < U - 1; ++u)
+        if (u < rem) a = __builtin_fmaf(v[u], wsh[k + u], a);
+    }
+  }
+  part[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int q = 1; q < S; ++q) t = t + part[q][lane];
+    if (!(flags & FEDAGG_INIT)) t = acc_in[c] + t;
+    if (flags & FEDAGG_FINALIZE) t = t / W32;
+    if (ok) epi.one(c0, t);
   }
 }
 
@@ -889,7 +957,8 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (B > 0 && !w) return FEDAGG_EINVAL;
   if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
-                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_MAP_MASK))
+                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_MAP_MASK |
+                FEDAGG_FAST))
     return FEDAGG_EINVAL;
   if (((flags & FEDAGG_MAP_MASK) >> FEDAGG_MAP_SHIFT) > 4) return FEDAGG_EINVAL;
   return 0;
@@ -983,6 +1052,46 @@ hipError_t launch_narrow_step(const NR& rows, int vw, const float* w, int64_t B,
 }
 
 
+// FEDAGG_FAST: waves per workgroup for the split-K kernel (enough for ~4096
+// waves), or 0 when one column per lane already gives a wave per SIMD: from
+// there on the exact kernels are as fast or faster (tools/bench_fast.py:
+// P = 199,210, K = 1000: exact 6.1 TB/s, split-K 5.1) and FEDAGG_FAST changes
+// nothing.
+int fast_split(int flags, int64_t P) {
+  if (!(flags & FEDAGG_FAST)) return 0;
+  const int64_t tiles = (P + 63) / 64;
+  if (tiles >= 1024) return 0;
+  int S = 2;
+  while (S < 16 && tiles * S < 4096) S *= 2;
+  return S;
+}
+
+template <class NR, class Epi>
+hipError_t launch_splitk(const NR& rows, int S, const float* w, int64_t B, int64_t P,
+                         const float* acc_in, const Epi& epi, float W32, int flags,
+                         hipStream_t s) {
+  const dim3 g(static_cast<unsigned>((P + 63) / 64));
+  switch (S) {
+    case 2:
+      hipLaunchKernelGGL((k_reduce_splitk<2, 8, true, NR, Epi>), g, dim3(128), 0, s, rows, w, B,
+                         P, acc_in, epi, W32, flags);
+      break;
+    case 4:
+      hipLaunchKernelGGL((k_reduce_splitk<4, 8, true, NR, Epi>), g, dim3(256), 0, s, rows, w, B,
+                         P, acc_in, epi, W32, flags);
+      break;
+    case 8:
+      hipLaunchKernelGGL((k_reduce_splitk<8, 8, true, NR, Epi>), g, dim3(512), 0, s, rows, w, B,
+                         P, acc_in, epi, W32, flags);
+      break;
+    default:
+      hipLaunchKernelGGL((k_reduce_splitk<16, 8, true, NR, Epi>), g, dim3(1024), 0, s, rows, w,
+                         B, P, acc_in, epi, W32, flags);
+      break;
+  }
+  return hipGetLastError();
+}
+
 // Column-block widths the blocked kernels are built for (one workgroup's span
 // of the wide mapping; a multiple of the narrow mapping's 256 * 2 columns).
 inline bool valid_block_cols(int64_t C) { return C == 1024 || C == 2048 || C == 4096; }
@@ -1067,6 +1176,9 @@ int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B, in
                          : max_cols_per_lane(P, {X, reinterpret_cast<const void*>(ldx * 4), out,
                                                  init ? nullptr : acc_in});
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (const int S = fast_split(flags, P))
+    return static_cast<int>(launch_splitk(NarrowStrided{X, ldx}, S, w, B, P, acc_in,
+                                          EpiStore{out}, W32, flags, s));
   // misaligned rows take the one-column-per-lane kernel whatever the mapping
   const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
   if (vw) return static_cast<int>(launch_narrow_store(NarrowStrided{X, ldx}, vw, w, B, P, acc_in,
@@ -1089,6 +1201,9 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
                          ? 1
                          : max_cols_per_lane(P, {out, init ? nullptr : acc_in});
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (const int S = fast_split(flags, P))
+    return static_cast<int>(launch_splitk(NarrowTable{rows, table_row_bytes(P)}, S, w, B, P,
+                                          acc_in, EpiStore{out}, W32, flags, s));
   const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
   if (vw)
     return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B, P,
@@ -1121,7 +1236,11 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
                                                                                  : acc_in}));
   // buffer-descriptor path unless asked for flat loads or a block region is
   // too large for a 32-bit descriptor range
-  if (vw) {
+  const int S = region32 && !(flags & (FEDAGG_LDSW | FEDAGG_FLAT)) ? fast_split(flags, P) : 0;
+  if (S) {
+    e = launch_splitk(NarrowBlocked{Xb, Kcap, C}, S, w, B, P, acc_in, EpiStore{out}, W32, flags,
+                      s);
+  } else if (vw) {
     e = launch_narrow_store(NarrowBlocked{Xb, Kcap, C}, vw, w, B, P, acc_in, out, W32, flags, s);
   } else if (flags & FEDAGG_LDSW) {
     // ablation: only the default configuration (C=4096, 256 lanes, U=4, nt)
@@ -1256,7 +1375,9 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
   // the per-C default configuration of fedagg_reduce_blocked_f32 (256 lanes,
   // VPT = C/1024, U = 4 at C=4096 else 2, non-temporal loads), or the narrow
   // mapping at small P
+  const int S = fast_split(flags, P);
   hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+    if (S) return launch_splitk(NarrowBlocked{Xb, Kcap, C}, S, w, B, P, acc_in, epi, W32, flags, s);
     if (vw)
       return launch_narrow_step(NarrowBlocked{Xb, Kcap, C}, vw, w, B, P, acc_in, epi, W32, flags,
                                 s);
@@ -1295,9 +1416,11 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   // allocations, read through buffer descriptors unless FEDAGG_FLAT
   const bool nt = (flags & FEDAGG_NT) != 0;
   const int vw = narrow_vw(flags, P, B, max_cols_per_lane(P, {}));  // operands 16-B aligned
-  if (vw) {
+  const int S = fast_split(flags, P);
+  if (vw || S) {
     const NarrowTable tab{rows, table_row_bytes(P)};
     hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+      if (S) return launch_splitk(tab, S, w, B, P, acc_in, epi, W32, flags, s);
       return launch_narrow_step(tab, vw, w, B, P, acc_in, epi, W32, flags, s);
     });
     if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _native
-from ._native import FEDAGG_FINALIZE, FEDAGG_INIT, FEDAGG_NT, FEDAGG_SCALAR, check
+from ._native import FEDAGG_FAST, FEDAGG_FINALIZE, FEDAGG_INIT, FEDAGG_NT, FEDAGG_SCALAR, check
 
 __all__ = [
     "fl32",
@@ -40,14 +40,16 @@ def fl32(x) -> float:
 
 
 def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
-                 flat: bool = False, ldsw: bool = False, mapping: str = "auto") -> int:
+                 flat: bool = False, ldsw: bool = False, mapping: str = "auto",
+                 fast: bool = False) -> int:
     """Kernel tuning bits (include/fedagg.h): k-unroll, float4 slots per lane
     (row-major / pointer-table layouts), non-temporal loads, the workgroup
     size of the column-blocked layout, flat (instead of buffer-descriptor)
     loads for it, and the column mapping (``"auto"``, ``"wide"`` = f32x4
     slots, ``"narrow1"`` / ``"narrow2"`` / ``"narrow4"`` = one / two / four
     columns per lane).
-    0 / False / "auto" = library default."""
+    ``fast``: FEDAGG_FAST, the reordered split-K mode for small P (normwise
+    parity, not bitwise).  0 / False / "auto" = library default."""
     sel = {0: 0, 4: 1, 8: 2, 16: 3, 2: 4, 32: 5}[unroll]
     msel = {"auto": 0, "wide": 1, "narrow1": 2, "narrow2": 3, "narrow4": 4}[mapping]
     vsel = {0: 0, 1: 1, 2: 2, 4: 3}[vpt]
@@ -55,7 +57,7 @@ def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
     return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
             | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0)
             | (_native.FEDAGG_FLAT if flat else 0) | (_native.FEDAGG_LDSW if ldsw else 0)
-            | (msel << _native.FEDAGG_MAP_SHIFT))
+            | (msel << _native.FEDAGG_MAP_SHIFT) | (_native.FEDAGG_FAST if fast else 0))
 
 
 # Tuned defaults for the column-blocked reduce (profiles/r01_sweep*/: K=1000 at
@@ -429,10 +431,12 @@ def reduce_blocked_step(
     r0: int = 0,
     mapping: str = "auto",
     unroll: int = 0,
+    flags: int = 0,
 ) -> torch.Tensor:
     """reduce_blocked(..., out=avg) then step.apply(avg), fused into one pass
     (fedagg_reduce_step_blocked_f32).  Returns step.cloud.  ``mapping`` as in
-    :func:`tuning_flags` (same results)."""
+    :func:`tuning_flags` (same results); ``flags``: further tuning bits
+    (e.g. FEDAGG_FAST) OR'ed in."""
     _require_hip_f32(Xb, "Xb")
     _require_hip_f32(w32, "w32")
     if Xb.dim() != 3 or not Xb.is_contiguous():
@@ -446,7 +450,7 @@ def reduce_blocked_step(
         raise ValueError("w32 too short")
     if r0 < 0 or B < 0 or r0 + B > Kcap:
         raise ValueError("row range outside the slab")
-    f = tuning_flags(unroll=unroll, mapping=mapping)
+    f = tuning_flags(unroll=unroll, mapping=mapping) | flags
     if acc_in is None:
         f |= FEDAGG_INIT
     else:
@@ -484,6 +488,7 @@ def reduce_rows_step(
     mapping: str = "auto",
     unroll: int = 0,
     checked: bool = False,
+    flags: int = 0,
 ) -> torch.Tensor:
     """reduce_rows(rows, ..., out=avg) then step.apply(avg), fused into one
     pass over the caller's own client tensors (fedagg_reduce_step_rows_f32):
@@ -505,7 +510,7 @@ def reduce_rows_step(
         raise ValueError("w32 too short")
     if not step.aligned():
         raise ValueError("every server-step operand must be 16-B aligned")
-    f = (FEDAGG_NT if nt else 0) | tuning_flags(flat=flat, mapping=mapping, unroll=unroll)
+    f = (FEDAGG_NT if nt else 0) | tuning_flags(flat=flat, mapping=mapping, unroll=unroll) | flags
     if acc_in is None:
         f |= FEDAGG_INIT
     else:

@@ -125,10 +125,10 @@ class _Ingest(object):
 
 class _Options(object):
     __slots__ = ("device", "slab_bytes", "max_rows", "flags", "expected_rows", "block_cols",
-                 "borrow")
+                 "borrow", "fast")
 
     def __init__(self, device, slab_bytes, max_rows, flags, expected_rows, block_cols,
-                 borrow=False):
+                 borrow=False, fast=False):
         self.device = device
         self.slab_bytes = slab_bytes
         self.max_rows = max_rows
@@ -136,6 +136,7 @@ class _Options(object):
         self.expected_rows = expected_rows
         self.block_cols = block_cols
         self.borrow = borrow
+        self.fast = fast
 
 
 class _DeviceEntry(object):
@@ -161,6 +162,8 @@ class _DeviceEntry(object):
         self.slab: Optional[torch.Tensor] = None
         self.hint = opts.expected_rows
         self.flags = ops.default_flags(self.C) if opts.flags is None else opts.flags
+        if opts.fast:
+            self.flags |= ops.FEDAGG_FAST
         self.agg = agg
         self.head = 0
         self.tail = 0
@@ -257,13 +260,14 @@ class _DeviceEntry(object):
         # every row passed _borrowable at add: skip the per-row checks
         if step is not None:
             ops.reduce_rows_step(rows, w32, step, acc_in=self.acc, W=final_W, table=table,
-                                 checked=True)
+                                 checked=True, flags=self.flags & ops.FEDAGG_FAST)
         else:
             acc_in = self.acc
             if self.acc is None:
                 self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
             ops.reduce_rows(rows, w32, self.acc, acc_in=acc_in, W=final_W,
-                            flags=ops.FEDAGG_NT, table=table, checked=True)
+                            flags=ops.FEDAGG_NT | (self.flags & ops.FEDAGG_FAST), table=table,
+                            checked=True)
         for t in rows:  # the caller's allocations may belong to another stream
             t.record_stream(cur)
         self.borrowed = []
@@ -296,7 +300,8 @@ class _DeviceEntry(object):
             last = i == len(segs) - 1
             if last and step is not None:
                 ops.reduce_blocked_step(self.slab, w32[off:off + cnt], step, B=cnt,
-                                        acc_in=acc_in, W=final_W, r0=r0)
+                                        acc_in=acc_in, W=final_W, r0=r0,
+                                        flags=self.flags & ops.FEDAGG_FAST)
             else:
                 if self.acc is None:
                     self.acc = torch.empty(self.P, dtype=torch.float32, device=self.dev)
@@ -375,15 +380,21 @@ class SerialAggregator(object):
             reduction raise (torch's version counter is checked).  The round
             driver enables it, since its client messages are dropped right
             after ``receive_from_client``.
+        fast: for models too small for one column per lane to fill the chip
+            (P below 65,536), split each column's K clients over several waves
+            (FEDAGG_FAST).  Deterministic, but the summation order is no longer
+            the reference's: results match it normwise (<= 1e-6 relative), not
+            bit for bit.  No effect at larger P.
     """
 
     def __init__(self, device=None, slab_bytes: Optional[int] = _DEFAULT_SLAB_BYTES,
                  max_rows: int = _DEFAULT_MAX_ROWS, flags: Optional[int] = None,
                  expected_rows: Optional[int] = None,
-                 block_cols: Optional[int] = None, borrow: bool = False) -> None:
+                 block_cols: Optional[int] = None, borrow: bool = False,
+                 fast: bool = False) -> None:
         self._members: Dict = dict()
         self._opts = _Options(device, slab_bytes, max_rows, flags, expected_rows, block_cols,
-                              borrow)
+                              borrow, fast)
         self._ingests: Dict = {}
 
     def _ingest(self, dev) -> _Ingest:

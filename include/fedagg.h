@@ -92,6 +92,14 @@ extern "C" {
  * allow them).  Same results. */
 #define FEDAGG_MAP_SHIFT 18
 #define FEDAGG_MAP_MASK  0x1C0000
+/* FAST (reordered) mode: when P is too small for one column per lane to fill
+ * the chip (below 65,536 columns), split the K rows of each 64-column tile over
+ * up to 16 waves of a workgroup (per-client weights staged in LDS, fmaf partial
+ * sums combined through LDS in a fixed order).  Deterministic, but NOT the
+ * reference's summation order: parity is normwise (<= 1e-6 relative and the
+ * gamma_K forward-error bound), not bitwise.  Ignored (exact kernels) where it
+ * would not add parallelism. */
+#define FEDAGG_FAST     0x200000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
