@@ -7,6 +7,12 @@ into the host-side receive loop and the rest, for client vectors that are
   device_borrow   HBM-resident tensors handed over (the round driver's default)
   device_snap     HBM-resident tensors snapshotted at add (borrow=False)
   host_pinned     pinned host tensors (CPU-side local trainers)
+  host_pageable   pageable host tensors (what vectorize_module returns on CPU)
+  cpu_run         pageable host tensors AND the cloud on the host: FedSim's
+                  device="cpu" run (config 1), aggregation on the MI355X; timed
+                  beside the reference's own CPU arithmetic for the same round
+                  (oracle/reference_loop.py: clone + mul + add per client,
+                  divide, then cloud - avg and the SGD step, torch CPU)
 
 and, for reference, the device-resident kernel time of the same reduce + step
 (tools/bench_configs.py).
@@ -41,6 +47,8 @@ def messages(K, P, where, dev, seed=11):
         t = torch.empty(P, device=dev).normal_(0.0, 0.05, generator=g)
         if where == "host_pinned":
             t = t.cpu().pin_memory()
+        elif where in ("host_pageable", "cpu_run"):
+            t = t.cpu()
         msgs.append(dict(local_params=t, num_steps=1, diverged=False,
                          num_samples={"train": weights[k]},
                          metrics={"train": {"cross_entropy_score": 1.0 + 1e-3 * k}}))
@@ -64,6 +72,28 @@ def one_round(msgs, cloud, borrow):
     return t1 - t0, t2 - t0
 
 
+def reference_round(msgs, P, reps=3):
+    """The reference's arithmetic for the same round on the host (oracle leg):
+    serial_aggregation's clone + SerialAggregator's mul/add per client, the
+    divide, then FedAvg.optimize's cloud - avg and SGD(lr=1) step."""
+    from oracle.reference_loop import aggregate_round
+
+    rows = [m["local_params"] for m in msgs]
+    weights = [m["num_samples"]["train"] for m in msgs]
+    best = None
+    for _ in range(reps):
+        cloud = torch.zeros(P, requires_grad=True)
+        opt = torch.optim.SGD(params=[cloud], lr=1.0)
+        t0 = time.perf_counter()
+        avg = aggregate_round(rows, weights)
+        opt.zero_grad()
+        cloud.grad = cloud.data - avg
+        opt.step()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -76,15 +106,20 @@ def main():
         K, P = CONFIGS[name]
         res = dict(K=K, P=P)
         for where, borrow in (("device_borrow", True), ("device_snap", False),
-                              ("host_pinned", False)):
+                              ("host_pinned", False), ("host_pageable", False),
+                              ("cpu_run", False)):
             msgs = messages(K, P, where, dev)
-            cloud = torch.zeros(P, device=dev, requires_grad=True)
+            cloud = torch.zeros(P, device="cpu" if where == "cpu_run" else dev,
+                                requires_grad=True)
             one_round(msgs, cloud, borrow)  # warm-up
             runs = [one_round(msgs, cloud, borrow) for _ in range(a.reps)]
             recv, total = min(r[0] for r in runs), min(r[1] for r in runs)
             res[where] = dict(round_ms=total * 1e3, receive_loop_ms=recv * 1e3,
                               per_client_us=recv / K * 1e6,
                               client_GBps=4.0 * K * P / total / 1e9)
+            if where == "cpu_run":
+                res["reference_cpu_round_ms"] = reference_round(msgs, P) * 1e3
+                res["cpu_threads"] = torch.get_num_threads()
             del msgs, cloud
             torch.cuda.empty_cache()
         out[name] = res

@@ -21,11 +21,13 @@ def main():
     ap.add_argument("--K", type=int, default=1000)
     ap.add_argument("--P", type=int, default=1_085_668)
     ap.add_argument("--borrow", type=int, default=1)
+    ap.add_argument("--where", default=None,
+                    help="device_borrow | device_snap | host_pinned | host_pageable | cpu_run")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    where = "device_borrow" if a.borrow else "device_snap"
+    where = a.where or ("device_borrow" if a.borrow else "device_snap")
     msgs = messages(a.K, a.P, where, dev)
-    cloud = torch.zeros(a.P, device=dev, requires_grad=True)
+    cloud = torch.zeros(a.P, device="cpu" if where == "cpu_run" else dev, requires_grad=True)
     for _ in range(2):
         one_round(msgs, cloud, bool(a.borrow))
     pr = cProfile.Profile()
