@@ -563,6 +563,28 @@ struct NarrowTable {
   }
 };
 
+// Row-pointer table with flat loads, for rows a descriptor cannot cover: its
+// range check is on the access's end, so a row of exactly 2^32 bytes
+// (P = 2^30, the largest P accepted) would read its last columns as zero.
+struct NarrowTableFlat {
+  const float* const* rows;
+  template <int VW>
+  __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
+    return static_cast<uint32_t>(c) * 4u;
+  }
+  template <int VW, bool NT, int SPAN = kBlock * VW>
+  __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
+    static_assert(VW == 1, "flat table rows: one column per lane");
+    Cols<VW> o;
+    o.v[0] = ld1<NT>(reinterpret_cast<const char*>(rows[k]), voff);
+    return o;
+  }
+};
+
+// A row's byte length fits one buffer descriptor (num_records is 32 bits and
+// checked against the access's end).
+inline bool row_fits_descriptor(int64_t P) { return P * 4 <= int64_t(0xFFFFFFFF); }
+
 // Row-major [B, ldx] slab (may exceed a descriptor's 4 GiB range): flat loads.
 struct NarrowStrided {
   const float* X;
@@ -941,8 +963,8 @@ hipError_t dispatch_blocked(const Rows& rows, int64_t C, int bs_sel, const float
   return hipErrorInvalidValue;
 }
 
-// num_records of a row's buffer descriptor: 4*P bytes, clamped to the 32-bit
-// field (P == 2^30 is the largest accepted size).
+// num_records of a row's buffer descriptor: 4*P bytes (rows that do not fit,
+// P = 2^30, take NarrowTableFlat; the clamp only keeps the value defined).
 uint32_t table_row_bytes(int64_t P) {
   const int64_t b = P * 4;
   return b >= (int64_t(1) << 32) ? 0xFFFFFFFFu : static_cast<uint32_t>(b);
@@ -1201,6 +1223,14 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
                          ? 1
                          : max_cols_per_lane(P, {out, init ? nullptr : acc_in});
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (!row_fits_descriptor(P)) {  // P = 2^30: flat loads, one column per lane
+    const EpiStore st{out};
+    return static_cast<int>(
+        (flags & FEDAGG_NT)
+            ? launch_narrow_t<8, 1, true>(NarrowTableFlat{rows}, w, B, P, acc_in, st, W32, flags, s)
+            : launch_narrow_t<8, 1, false>(NarrowTableFlat{rows}, w, B, P, acc_in, st, W32, flags,
+                                           s));
+  }
   if (const int S = fast_split(flags, P))
     return static_cast<int>(launch_splitk(NarrowTable{rows, table_row_bytes(P)}, S, w, B, P,
                                           acc_in, EpiStore{out}, W32, flags, s));
@@ -1415,6 +1445,14 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   // per lane, U = kRowsUnroll); the rows are the caller's separate
   // allocations, read through buffer descriptors unless FEDAGG_FLAT
   const bool nt = (flags & FEDAGG_NT) != 0;
+  if (!row_fits_descriptor(P)) {  // P = 2^30: flat loads, one column per lane
+    hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
+      return launch_narrow_t<8, 1, true>(NarrowTableFlat{rows}, w, B, P, acc_in, epi, W32, flags,
+                                         s);
+    });
+    if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
+    return static_cast<int>(e);
+  }
   const int vw = narrow_vw(flags, P, B, max_cols_per_lane(P, {}));  // operands 16-B aligned
   const int S = fast_split(flags, P);
   if (vw || S) {
