@@ -172,7 +172,41 @@ def cpu_baseline(P, budget_s):
     )
 
 
+class _StdoutToStderr(object):
+    """Route file descriptor 1 to stderr until the result line is printed,
+    so that banners written by native libraries (RCCL prints its version
+    block to stdout at communicator init) cannot join the ONE JSON line the
+    driver reads from stdout."""
+
+    def __init__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def restore(self):
+        if self.saved is None:
+            return
+        sys.stdout.flush()
+        try:  # C stdio buffers written while fd 1 was stderr go there too
+            import ctypes
+
+            ctypes.CDLL(None).fflush(None)
+        except (OSError, AttributeError):
+            pass
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        self.saved = None
+
+
 def main():
+    quiet = _StdoutToStderr()
+    try:
+        _main(quiet)
+    finally:
+        quiet.restore()
+
+
+def _main(quiet):
     a = parse()
     world, rank, local, dist = dist_setup()
     dev = torch.device("cuda", local)
@@ -291,6 +325,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(P, a.cpu_baseline_seconds)
     if rank == 0:
+        quiet.restore()
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.barrier()
