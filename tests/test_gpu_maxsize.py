@@ -66,3 +66,60 @@ def test_max_P_blocked_fused_step(data):
     got = cloud[d["idx"]].cpu().numpy()
     zero = np.zeros_like(d["want"])
     np.testing.assert_array_equal(bits(got), bits(ref.fedavg_sgd(d["want"], zero, 1.0)))
+
+
+@pytest.mark.parametrize("kcap", [(1 << 18) - 1, 1 << 18])
+def test_blocked_region_at_the_descriptor_limit(kcap):
+    """A column block's region (Kcap * C * 4 bytes) just under 4 GiB takes the
+    buffer-descriptor kernels, at 4 GiB the flat ones; rows at the very end of
+    the region, both column blocks (one ragged), against the oracle."""
+    from fedsim_amd import ops
+    from oracle import vectors as V
+
+    dev = torch.device("cuda:0")
+    C, Pc, B = 4096, 4096 + 5, 3
+    X = V.client_rows("realistic", B, Pc, 17)
+    w = V.client_weights("fedavg", B, 17)
+    Xb = torch.empty(ops.blocked_shape(kcap, Pc, C), dtype=torch.float32, device=dev)
+    r0 = kcap - B
+    for j in range(B):
+        ops.pack_row(torch.from_numpy(X[j].copy()).to(dev), Xb, r0 + j)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    out = torch.empty(Pc, dtype=torch.float32, device=dev)
+    want = ref.reduce(X, w, W=sum(w))
+    for mapping in ("auto", "wide", "narrow4"):
+        ops.reduce_blocked(Xb, w32, out, B=B, W=sum(w), r0=r0,
+                           flags=ops.tuning_flags(mapping=mapping))
+        np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(want))
+    del Xb
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("kcap", [(1 << 18) - 1, 1 << 18])
+def test_blocked_full_region_high_row_offsets(kcap):
+    """Every row of a region just under / at 4 GiB (row offsets up to ~4 GiB
+    in the 32-bit soffset), values in {0, 1} and weights 1 so that every
+    partial sum is an integer below 2^24 and the result is known exactly."""
+    from fedsim_amd import ops
+
+    dev = torch.device("cuda:0")
+    C, Pc = 4096, 4096 + 5
+    nb = 2
+    Xb = torch.empty((nb, kcap, C), dtype=torch.float32, device=dev)
+    k = torch.arange(kcap, dtype=torch.int32, device=dev).view(-1, 1)
+    for b in range(nb):
+        p = (b * C + torch.arange(C, dtype=torch.int32, device=dev)).view(1, -1)
+        Xb[b] = ((7 * k + p) % 3 == 0).float()
+    del k
+    w32 = torch.ones(kcap, dtype=torch.float32, device=dev)
+    cols = np.arange(Pc)
+    # k = -p (mod 3) for k in [0, kcap)
+    res = (-cols) % 3
+    count = (kcap - 1 - res) // 3 + 1
+    want = (count.astype(np.float32) / np.float32(kcap)).astype(np.float32)
+    out = torch.empty(Pc, dtype=torch.float32, device=dev)
+    for mapping in ("auto", "wide", "narrow4"):
+        ops.reduce_blocked(Xb, w32, out, W=kcap, flags=ops.tuning_flags(mapping=mapping))
+        np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(want))
+    del Xb
+    torch.cuda.empty_cache()
