@@ -56,6 +56,15 @@
 namespace {
 
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
+// Lanes per narrow-mapping workgroup: one wave.  A workgroup's share of the
+// rows is then 1/4 of a 256-lane one, so the dispatcher balances the tail of
+// the grid more finely: +1.4 % at 1000 x 25 M, +1.6 % at 1000 x 199,210, even
+// at 1.09 M / 3.125 M (tools/sweep_variants.py, profiles/r01as/, r01at/;
+// 512 / 1024 lanes were 0.5 / 2 % slower than 256).
+#ifndef FEDAGG_NARROW_BLOCK  // build-variant knob for those measurements
+#define FEDAGG_NARROW_BLOCK 64
+#endif
+constexpr int kNarrowBlock = FEDAGG_NARROW_BLOCK;
 // Tuned defaults (profiles/r01_*: K=1000 x P=25M sweep on MI355X).
 constexpr int kDefaultUnroll = 4;
 constexpr int kDefaultVptSel = 2;  // 2 float4 slots per lane
@@ -536,7 +545,7 @@ struct NarrowBlocked {
     return static_cast<uint32_t>(c & (C - 1)) * 4u;
   }
   // SPAN: columns one workgroup covers (all inside one block)
-  template <int VW, bool NT, int SPAN = kBlock * VW>
+  template <int VW, bool NT, int SPAN = kNarrowBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
     const int64_t b = (static_cast<int64_t>(blockIdx.x) * SPAN) >> __builtin_ctzll(C);
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
@@ -554,7 +563,7 @@ struct NarrowTable {
   __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
     return static_cast<uint32_t>(c) * 4u;
   }
-  template <int VW, bool NT, int SPAN = kBlock * VW>
+  template <int VW, bool NT, int SPAN = kNarrowBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(rows[k]), static_cast<short>(0), static_cast<int>(row_bytes),
@@ -572,7 +581,7 @@ struct NarrowTableFlat {
   __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
     return static_cast<uint32_t>(c) * 4u;
   }
-  template <int VW, bool NT, int SPAN = kBlock * VW>
+  template <int VW, bool NT, int SPAN = kNarrowBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
     static_assert(VW == 1, "flat table rows: one column per lane");
     Cols<VW> o;
@@ -593,7 +602,7 @@ struct NarrowStrided {
   __device__ __forceinline__ uint32_t lane_off(int64_t c) const {
     return static_cast<uint32_t>(c) * 4u;
   }
-  template <int VW, bool NT, int SPAN = kBlock * VW>
+  template <int VW, bool NT, int SPAN = kNarrowBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
     const char* p = reinterpret_cast<const char*>(X + k * ldx) + voff;
     Cols<VW> o;
@@ -614,11 +623,11 @@ struct NarrowStrided {
 };
 
 template <int U, int VW, bool NT, class NR, class Epi>
-__global__ __launch_bounds__(kBlock) void k_reduce_narrow(NR rows, const float* __restrict__ w,
+__global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const float* __restrict__ w,
                                                           int64_t B, int64_t P,
                                                           const float* acc_in, Epi epi,
                                                           float W32, int flags) {
-  const int64_t c0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * VW;
+  const int64_t c0 = (static_cast<int64_t>(blockIdx.x) * kNarrowBlock + threadIdx.x) * VW;
   const bool ok = c0 < P;
   const int64_t c = ok ? c0 : P - VW;  // clamp: load something valid, store nothing
   const uint32_t voff = rows.template lane_off<VW>(c);
@@ -1018,9 +1027,9 @@ template <int U, int VW, bool NT, class NR, class Epi>
 hipError_t launch_narrow_t(const NR& rows, const float* w, int64_t B, int64_t P,
                            const float* acc_in, const Epi& epi, float W32, int flags,
                            hipStream_t s) {
-  const int64_t grid = (P + kBlock * VW - 1) / (kBlock * VW);
+  const int64_t grid = (P + kNarrowBlock * VW - 1) / (kNarrowBlock * VW);
   hipLaunchKernelGGL((k_reduce_narrow<U, VW, NT, NR, Epi>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kBlock), 0, s, rows, w, B, P, acc_in, epi, W32, flags);
+                     dim3(kNarrowBlock), 0, s, rows, w, B, P, acc_in, epi, W32, flags);
   return hipGetLastError();
 }
 
@@ -1115,7 +1124,7 @@ hipError_t launch_splitk(const NR& rows, int S, const float* w, int64_t B, int64
 }
 
 // Column-block widths the blocked kernels are built for (one workgroup's span
-// of the wide mapping; a multiple of the narrow mapping's 256 * 2 columns).
+// of the wide mapping; a multiple of a narrow workgroup's kNarrowBlock * 4 columns).
 inline bool valid_block_cols(int64_t C) { return C == 1024 || C == 2048 || C == 4096; }
 
 // Validate a server step's operands and pack them for EpiStep.

@@ -87,7 +87,7 @@ extern "C" {
  * (narrow: one column per lane below P = 2^20, two from there on, four for
  * P >= 2^24 with at most 128 rows per call), 1 = wide
  * (f32x4 slots; the unroll / VPT / BS tuning bits apply to it), 2 / 3 / 4 =
- * narrow with one / two / four columns per lane (each workgroup 256 lanes;
+ * narrow with one / two / four columns per lane (each workgroup one wave;
  * falls back to fewer columns when P or an operand's alignment does not
  * allow them).  Same results. */
 #define FEDAGG_MAP_SHIFT 18

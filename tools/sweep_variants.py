@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--P", type=int, default=25_000_000)
     ap.add_argument("--C", type=int, default=4096)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variant-flags", default="",
+                    help="comma-separated extra flag words, one per library (tuning bits "
+                         "OR'ed into the fused call, e.g. ops.tuning_flags(unroll=16))")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--shape", default="", help="also time tools/shape_kernel.hip's probe .so")
     ap.add_argument("--fill", default="normal", choices=["normal", "const"],
@@ -54,27 +57,29 @@ def main():
     w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
     W32 = ops.fl32(sum(w))
     libs = [load(p) for p in a.libs]
+    vflags = [int(v, 0) for v in a.variant_flags.split(",")] if a.variant_flags else []
+    vflags += [0] * (len(libs) - len(vflags))
     stream = torch.cuda.current_stream(dev).cuda_stream
     cloud0 = torch.zeros(P, device=dev)
-    results = {p: [] for p in a.libs}
+    results = {i: [] for i in range(len(a.libs))}
     outs = {}
     alg = 4.0 * K * P + 4.0 * K + 12.0 * P
     for r in range(a.rounds):
-        for path, lib in zip(a.libs, libs):
+        for i, (path, lib, xf) in enumerate(zip(a.libs, libs, vflags)):
             cloud = cloud0.clone()
             grad = torch.empty(P, device=dev)
             step = ops.ServerStep("fedavg", cloud, lr=1.0, grad_out=grad)
 
             def run():
                 rc = lib.fedagg_reduce_step_blocked_f32(
-                    Xb.data_ptr(), K, C, w32.data_ptr(), K, P, None, W32, 0x1 | 0x2,
+                    Xb.data_ptr(), K, C, w32.data_ptr(), K, P, None, W32, 0x1 | 0x2 | xf,
                     ctypes.byref(step.args), stream)
                 assert rc == 0, rc
 
             run()
             torch.cuda.synchronize()
             if r == 0:
-                outs[path] = cloud.clone()
+                outs[i] = cloud.clone()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
@@ -82,7 +87,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
-            results[path].append(ms)
+            results[i].append(ms)
     # the plain reduce (no server step) of the first library: buffer-descriptor
     # loads (default) vs flat global loads (FEDAGG_FLAT), same slab
     avg = torch.empty(P, device=dev)
@@ -132,13 +137,14 @@ def main():
         print(json.dumps(dict(lib=os.path.basename(a.shape), kernel="shape (checksum only)",
                               ms_min=min(ts), GBps=4.0 * K * Xb.shape[0] * C / min(ts) / 1e6)),
               flush=True)
-    ref = outs[a.libs[0]]
-    for path in a.libs:
-        ms = min(results[path])
-        print(json.dumps(dict(lib=os.path.basename(path), ms_min=ms,
-                              ms_all=[round(x, 4) for x in results[path]],
+    ref = outs[0]
+    for i, path in enumerate(a.libs):
+        ms = min(results[i])
+        print(json.dumps(dict(lib=os.path.basename(path), flags=vflags[i], ms_min=ms,
+                              ms_median=float(np.median(results[i])),
+                              ms_all=[round(x, 4) for x in results[i]],
                               GBps=alg / ms / 1e6,
-                              bitwise_vs_first=bool(torch.equal(outs[path].view(torch.int32),
+                              bitwise_vs_first=bool(torch.equal(outs[i].view(torch.int32),
                                                                 ref.view(torch.int32))))),
               flush=True)
 
