@@ -147,3 +147,43 @@ def test_nonfinite_inputs(dev, C):
     exp = ref.reduce(X, w, W=W)
     assert np.isnan(exp[50:100]).all() and np.isposinf(exp[:50]).all()
     same(out.cpu().numpy(), exp)
+
+
+@SETTINGS
+@given(rounds(max_k=40, max_p=6000),
+       st.sampled_from(["wide", "narrow1", "narrow2", "narrow4"]),
+       st.sampled_from([0, 8, 16, 32]), st.sampled_from(["strided", "rows", "blocked"]),
+       st.integers(0, 3))
+def test_mapping_random(dev, r, mapping, unroll, layout, split):
+    """Every column mapping x unroll x layout on random shapes and values,
+    split into two chained calls at a random row, against the oracle."""
+    from fedsim_amd import ops
+
+    X, w = _accepted(*r)
+    K, P = X.shape
+    if K == 0:
+        return
+    W = sum(w)
+    h = min(K, split * K // 3)
+    u = unroll if mapping != "wide" else {0: 0, 8: 8, 16: 16, 32: 4}[unroll]
+    fl = ops.tuning_flags(mapping=mapping, unroll=u)
+    Xd = torch.from_numpy(X).to(dev)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    Xb = ops.to_blocked(Xd, 1024) if layout == "blocked" else None
+
+    def call(k0, k1, acc, fin):
+        kw = dict(acc_in=acc, W=W if fin else None, flags=fl)
+        if layout == "strided":
+            ops.reduce_slab(Xd[k0:k1], w32[k0:k1].contiguous(), out, **kw)
+        elif layout == "rows":
+            ops.reduce_rows([Xd[k] for k in range(k0, k1)], w32[k0:k1].contiguous(), out, **kw)
+        else:
+            ops.reduce_blocked(Xb, w32[k0:k1].contiguous(), out, B=k1 - k0, r0=k0, **kw)
+
+    if h:
+        call(0, h, None, False)
+        call(h, K, out, True)
+    else:
+        call(0, K, None, True)
+    same(out.cpu().numpy(), ref.reduce(X, w, W=W))
