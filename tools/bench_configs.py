@@ -44,6 +44,23 @@ def timed(fn, steps, warmup=2):
     return (time.perf_counter() - t0) / steps
 
 
+def gpu_time(fn, steps):
+    """Median time of one isolated call between two HIP events on the current
+    stream, synchronized each time: includes the launch latency of an idle
+    GPU, which back-to-back calls (the wall-clock rate) overlap.  Kernel-only
+    times come from rocprofv3 or tools/sweep_variants.py."""
+    ms = []
+    for _ in range(steps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    return float(np.median(ms)) * 1e-3
+
+
 def round_exact(Xb, w32, W, P, epilogue=None, pool_passes=1, K_pool=None, fused=False):
     """One round: pool_passes reduce passes (+ divide in the last), then the
     server step.  fused=True runs the step inside the last pass
@@ -119,9 +136,11 @@ def main():
         w32 = torch.tensor([ops.fl32(v) for v in ws], device=dev)
         for fused in (True, False):
             fn, _ = round_exact(Xb, w32, sum(ws), P, epilogue=epi, fused=fused)
-            report(name + ("" if fused else "_split"), K, P, timed(fn, max(a.steps, 20)),
+            t = timed(fn, max(a.steps, 20))
+            gt = gpu_time(fn, max(a.steps, 20))
+            report(name + ("" if fused else "_split"), K, P, t,
                    dict(epilogue=epi, step="fused into the last reduce" if fused
-                        else "separate epilogue launch"))
+                        else "separate epilogue launch", isolated_call_ms=gt * 1e3))
         del Xb
 
     if "cfg4" in only:
