@@ -16,8 +16,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedsim_amd import ops  # noqa: E402
 
-VARIANTS = [("wide", 0), ("narrow2", 8), ("narrow2", 16), ("narrow4", 8), ("narrow4", 16),
-            ("narrow1", 8), ("narrow1", 16)]
+VARIANTS = [("auto", 0), ("wide", 0), ("narrow2", 8), ("narrow2", 16), ("narrow2", 32),
+            ("narrow4", 8), ("narrow4", 16), ("narrow1", 8), ("narrow1", 16), ("narrow1", 32)]
 
 
 def main():
