@@ -1125,7 +1125,11 @@ hipError_t launch_splitk(const NR& rows, int S, const float* w, int64_t B, int64
 
 // Column-block widths the blocked kernels are built for (one workgroup's span
 // of the wide mapping; a multiple of a narrow workgroup's kNarrowBlock * 4 columns).
+#ifdef FEDAGG_ANY_C  // layout experiments (tools/ab_small_c.py): any power of two 128..16384
+inline bool valid_block_cols(int64_t C) { return C >= 128 && C <= 16384 && !(C & (C - 1)); }
+#else
 inline bool valid_block_cols(int64_t C) { return C == 1024 || C == 2048 || C == 4096; }
+#endif
 
 // Validate a server step's operands and pack them for EpiStep.
 int make_step(int algo, float coef, float* cloud, float* aux, float* avg_prev, float* buf,

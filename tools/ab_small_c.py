@@ -2,11 +2,11 @@
 columns per lane, one one-wave workgroup owns a whole column block, so it
 streams one contiguous K*512-byte region (the "small per-workgroup chunks"
 regime of the read-stream probes).  Needs a build with
--DFEDAGG_SMALL_C (valid_block_cols admits 128..4096).  Fused FedAvg round,
+-DFEDAGG_ANY_C (valid_block_cols admits 128..16384).  Fused FedAvg round,
 forced narrow mappings, one slab allocation reinterpreted per C, interleaved.
 Timing only: the slab's logical contents differ per C.
 
-python tools/ab_small_c.py tools/variants/libfedagg_smallc.so [--K 1000] [--P 25000000]
+python tools/ab_small_c.py tools/variants/libfedagg_anyc.so [--K 1000] [--P 25000000]
 """
 import argparse
 import ctypes
