@@ -533,6 +533,21 @@ __device__ __forceinline__ Cols<VW> buf_load_cols(__amdgpu_buffer_rsrc_t r, uint
   return o;
 }
 
+// Row-address prefetch for k_reduce_narrow's main loop.  Policies whose row
+// address is arithmetic have nothing to fetch; the pointer-table policy loads
+// the next batch's U row pointers while the current batch's rows stream.
+struct NoRowPrefetch {};
+#define FEDAGG_NO_ROW_PREFETCH                                                              \
+  template <int U>                                                                          \
+  __device__ __forceinline__ NoRowPrefetch prefetch(int64_t) const {                        \
+    return {};                                                                              \
+  }                                                                                         \
+  template <int VW, bool NT, int U>                                                         \
+  __device__ __forceinline__ Cols<VW> load_at(const NoRowPrefetch&, int64_t k, int u,       \
+                                              uint32_t voff) const {                        \
+    return load<VW, NT>(k + u, voff);                                                       \
+  }
+
 // Column-blocked slab: the workgroup's 256*VW columns lie in one column block
 // b (C is a multiple of 256*VW); its region is one buffer descriptor, the row
 // an SGPR soffset, the lane's column-in-block a VGPR voffset.
@@ -552,7 +567,7 @@ struct NarrowBlocked {
         const_cast<float*>(X + b * Kcap * C), static_cast<short>(0),
         static_cast<int>(static_cast<uint32_t>(Kcap * C * 4)), 0x00020000);
     return buf_load_cols<VW, NT>(r, voff, static_cast<uint32_t>(k) * static_cast<uint32_t>(C * 4));
-  }
+  }  FEDAGG_NO_ROW_PREFETCH
 };
 
 // Row-pointer table: one descriptor per row (wave-uniform scalar load).
@@ -565,9 +580,29 @@ struct NarrowTable {
   }
   template <int VW, bool NT, int SPAN = kNarrowBlock * VW>
   __device__ __forceinline__ Cols<VW> load(int64_t k, uint32_t voff) const {
+    return load_row<VW, NT>(rows[k], voff);
+  }
+  template <int U>
+  struct Batch {
+    const float* p[U];
+  };
+  // the U row pointers of rows k .. k+U-1 (scalar loads, in SGPRs)
+  template <int U>
+  __device__ __forceinline__ Batch<U> prefetch(int64_t k) const {
+    Batch<U> b;
+#pragma unroll
+    for (int u = 0; u < U; ++u) b.p[u] = rows[k + u];
+    return b;
+  }
+  template <int VW, bool NT, int U>
+  __device__ __forceinline__ Cols<VW> load_at(const Batch<U>& b, int64_t, int u,
+                                              uint32_t voff) const {
+    return load_row<VW, NT>(b.p[u], voff);
+  }
+  template <int VW, bool NT>
+  __device__ __forceinline__ Cols<VW> load_row(const float* row, uint32_t voff) const {
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(rows[k]), static_cast<short>(0), static_cast<int>(row_bytes),
-        0x00020000);
+        const_cast<float*>(row), static_cast<short>(0), static_cast<int>(row_bytes), 0x00020000);
     return buf_load_cols<VW, NT>(r, voff, 0u);
   }
 };
@@ -587,7 +622,7 @@ struct NarrowTableFlat {
     Cols<VW> o;
     o.v[0] = ld1<NT>(reinterpret_cast<const char*>(rows[k]), voff);
     return o;
-  }
+  }  FEDAGG_NO_ROW_PREFETCH
 };
 
 // A row's byte length fits one buffer descriptor (num_records is 32 bits and
@@ -619,7 +654,7 @@ struct NarrowStrided {
       for (int e = 0; e < 4; ++e) o.v[e] = t[e];
     }
     return o;
-  }
+  }  FEDAGG_NO_ROW_PREFETCH
 };
 
 template <int U, int VW, bool NT, class NR, class Epi>
@@ -635,10 +670,16 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
 #pragma unroll
   for (int e = 0; e < VW; ++e) a[e] = (flags & FEDAGG_INIT) ? 0.f : acc_in[c + e];
   int64_t k = 0;
+  // row addresses of the next batch are fetched while this batch streams
+  // (clamped to the last full batch, so the table is never over-read)
+  decltype(rows.template prefetch<U>(0)) next{};
+  if (U <= B) next = rows.template prefetch<U>(0);
   for (; k + U <= B; k += U) {
+    const auto cur = next;
     Cols<VW> v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = rows.template load<VW, NT>(k + u, voff);
+    for (int u = 0; u < U; ++u) v[u] = rows.template load_at<VW, NT, U>(cur, k, u, voff);
+    next = rows.template prefetch<U>(k + 2 * U <= B ? k + U : k);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float wk = w[k + u];
