@@ -79,12 +79,13 @@ constexpr int kWeightTile = 2048;  // FEDAGG_LDSW ablation: weights per LDS tile
 //  * P >= 2^20: two columns per lane, U = 16 (U = 8 from 2^24 on), even with
 //    or ahead of the tuned f32x4 kernels: +0.5..1.3 % at 1000 x 25 M, +3.8 %
 //    at 1000 x 6.25 M, +3.8..5.7 % at 10,000 x 3.125 M (config 4's shard);
-//  * P >= 2^24 with few rows per launch (B <= 128, e.g. config 5's 100-row
-//    pool passes): four columns per lane, U = 8 (+3 % over two at 100 x 125 M:
-//    a workgroup's fixed costs are spread over few rows there).
+//  * P >= 2^24 with few rows per launch (B <= 64): four columns per lane,
+//    U = 8 (a workgroup's fixed costs are spread over few rows there).  Under
+//    one-wave workgroups two columns win again from about B = 100 (+2.7 % at
+//    100 x 125 M, +3.5 % at 128 x 25 M, +5 % at 128 x 2^24; profiles/r01bo/).
 constexpr int64_t kNarrowWideP = int64_t(1) << 20;
 constexpr int64_t kNarrowLongP = int64_t(1) << 24;
-constexpr int64_t kNarrowShortB = 128;
+constexpr int64_t kNarrowShortB = 64;
 
 // Native clang vector (HIP's float4 is a struct and cannot feed the
 // nontemporal builtin).

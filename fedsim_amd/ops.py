@@ -421,6 +421,26 @@ def can_fuse_step(Xb: torch.Tensor, step: ServerStep) -> bool:
             and Xb.device == step.cloud.device)
 
 
+# Below 2^24 columns the narrow kernels' grid is a few generations of resident
+# waves, and a wave that carries the server step ends with a dependent load of
+# the step's operands (cloud / aux) that keeps its slot idle: with B >= 128
+# rows the separate epilogue launch is 1-7 % faster than the fused one there
+# (profiles/r01bq/, r01br/, r01bs/; slab and borrowed rows, FedAvg and
+# AdaBest), in spite of the 8 P bytes of the stored average.  Fewer rows pay
+# more for the extra launch than the epilogue costs; from 2^24 columns on the
+# two measure within noise and the fused pass saves the 8 P bytes.
+_SPLIT_STEP_MIN_P = 1 << 20
+_SPLIT_STEP_MAX_P = 1 << 24
+_SPLIT_STEP_MIN_B = 128
+
+
+def fuse_step_pays(P: int, B: int) -> bool:
+    """Whether the last drain of a round should run the server step fused
+    (fedagg_reduce_step_*_f32) rather than store the average and run
+    fedagg_server_step_f32 after it.  Same results either way (bitwise)."""
+    return not (_SPLIT_STEP_MIN_P <= P < _SPLIT_STEP_MAX_P and B >= _SPLIT_STEP_MIN_B)
+
+
 def reduce_blocked_step(
     Xb: torch.Tensor,
     w32: torch.Tensor,

@@ -366,12 +366,15 @@ class _DeviceEntry(object):
 
     def pop_step(self, step: ops.ServerStep) -> None:
         """pop(on_device=True) followed by step.apply(avg), fused into the last
-        drain when rows are pending and the step's operands allow it."""
+        drain when rows are pending, the step's operands allow it and the
+        fused pass is the faster one at this size (ops.fuse_step_pays)."""
         if self.borrowed:
             fusable = step.aligned() and step.cloud.device == self.dev
+            rows = len(self.borrowed)
         else:
             fusable = self.n_pending > 0 and ops.can_fuse_step(self.slab, step)
-        if not fusable:
+            rows = self.n_pending
+        if not fusable or not ops.fuse_step_pays(self.P, rows):
             step.apply(self.pop(on_device=True).reshape(-1))
             return
         self._flush(final_W=self.cur_w if self._weighted() else None, step=step)

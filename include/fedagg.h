@@ -85,7 +85,7 @@ extern "C" {
  * sum is parallel over columns only, so at small P the f32x4-slot ("wide")
  * kernels leave CUs idle (P = 199,210 is 778 waves).  0 = library default
  * (narrow: one column per lane below P = 2^20, two from there on, four for
- * P >= 2^24 with at most 128 rows per call), 1 = wide
+ * P >= 2^24 with at most 64 rows per call), 1 = wide
  * (f32x4 slots; the unroll / VPT / BS tuning bits apply to it), 2 / 3 / 4 =
  * narrow with one / two / four columns per lane (each workgroup one wave;
  * falls back to fewer columns when P or an operand's alignment does not

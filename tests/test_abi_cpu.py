@@ -153,6 +153,20 @@ def test_build_is_gfx950():
     assert ctypes.sizeof(ctypes.c_void_p) == 8
 
 
+def test_fuse_step_policy():
+    """ops.fuse_step_pays: the last drain runs the server step fused except at
+    2^20 <= P < 2^24 with >= 128 rows (profiles/r01bq/, r01br/, r01bs/)."""
+    from fedsim_amd import ops
+
+    assert ops.fuse_step_pays(25_000_000, 1000)       # headline: fused
+    assert ops.fuse_step_pays(199_210, 1000)          # narrow1 sizes: fused
+    assert ops.fuse_step_pays(1_085_668, 10)          # few rows: one launch
+    assert ops.fuse_step_pays(1_085_668, 127)
+    assert not ops.fuse_step_pays(1_085_668, 128)     # SimpleCNN2 x 1000 clients: split
+    assert not ops.fuse_step_pays((1 << 24) - 1, 1000)
+    assert ops.fuse_step_pays(1 << 24, 1000)
+
+
 def test_column_mapping_decision():
     """fedagg_column_mapping: the library's default mapping per P (narrow, one
     column per lane below 2^20, two from there on; unroll 8 / 16 / 8) and the
@@ -162,8 +176,9 @@ def test_column_mapping_decision():
     assert ops.column_mapping(199_210) == ("narrow1", 8)
     assert ops.column_mapping(1_085_668) == ("narrow2", 16)
     assert ops.column_mapping(25_000_000) == ("narrow2", 8)
-    assert ops.column_mapping(125_000_000, B=100) == ("narrow4", 8)  # short pool passes
-    assert ops.column_mapping(125_000_000, B=129) == ("narrow2", 8)
+    assert ops.column_mapping(125_000_000, B=64) == ("narrow4", 8)  # short launches
+    assert ops.column_mapping(125_000_000, B=65) == ("narrow2", 8)
+    assert ops.column_mapping(125_000_000, B=100) == ("narrow2", 8)  # profiles/r01bo/
     assert ops.column_mapping(1_085_668, B=100) == ("narrow2", 16)
     assert ops.column_mapping(25_000_000, max_vw=1) == ("narrow1", 8)
     assert ops.column_mapping(25_000_001) == ("narrow1", 8)  # odd P: one column per lane

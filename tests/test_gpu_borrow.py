@@ -214,3 +214,42 @@ def test_rows_step_mappings_bitwise(algo, mapping, P, dev):
     np.testing.assert_array_equal(bits(cloud.cpu().numpy()), bits(want.cloud))
     if algo != "fedavg":
         np.testing.assert_array_equal(bits(aux.cpu().numpy()), bits(want.aux))
+
+
+@pytest.mark.parametrize("borrow", [True, False])
+@pytest.mark.parametrize("algo", ["fedavg", "adabest"])
+def test_pop_step_split_policy_bitwise(borrow, algo, dev):
+    """At P in [2^20, 2^24) with >= 128 rows, pop_step stores the average and
+    runs fedagg_server_step_f32 after it (ops.fuse_step_pays): the result is
+    bit for bit the fused pass's, forced here through the library entry, and
+    the oracle's for plain FedAvg SGD."""
+    from fedsim_amd import ops
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 130, (1 << 20) + 6
+    assert not ops.fuse_step_pays(P, K)
+    X = V.client_rows("realistic", K, P, 12)
+    w = V.client_weights("fedavg", K, 12)
+    cloud0 = torch.from_numpy(V.cloud_vector(P, 13)).to(dev)
+    aux0 = torch.from_numpy(V.cloud_vector(P, 14)).to(dev)
+    rows = [torch.from_numpy(X[k].copy()).to(dev) for k in range(K)]
+    outs = []
+    for via in ("aggregator", "fused_entry"):
+        cloud, aux, grad = cloud0.clone(), aux0.clone(), torch.empty_like(cloud0)
+        step = ops.ServerStep(algo, cloud, lr=0.3, coef=0.6,
+                              aux=None if algo == "fedavg" else aux, grad_out=grad)
+        if via == "aggregator":
+            agg = SerialAggregator(borrow=borrow)
+            for k in range(K):
+                agg.add("p", rows[k], w[k])
+            agg.pop_step("p", step)
+        else:
+            w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
+            ops.reduce_rows_step(rows, w32, step, W=sum(w))
+        outs.append([t.cpu().numpy() for t in (cloud, aux, grad)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(bits(a), bits(b))
+    if algo == "fedavg":
+        avg = ref.reduce(X, w, W=sum(w))
+        np.testing.assert_array_equal(bits(outs[0][0]),
+                                      bits(ref.fedavg_sgd(avg, cloud0.cpu().numpy(), 0.3)))

@@ -7,7 +7,7 @@ K=1000 x P=25M line) with the sizes the reference's own configs use.
   cfg3  AdaBest beta=0.6, SimpleCNN2 P=1,085,668, K=10 / 1000 (w=1, AdaBest epilogue)
   cfg4  FedAvg synthetic, param-sharded: per-GPU shard K=10,000 x P=25M/8
   cfg5  FedAvg synthetic, client-sharded: per-GPU K=12,500 x P=125M streamed from a
-        resident 64-row pool (re-read cyclically), + RCCL all-reduce(4P) when N>1
+        resident 200-row pool (re-read cyclically), + RCCL all-reduce(4P) when N>1
 
 One process per GPU under torch.distributed.run for N>1 (cfg4/cfg5 only).
 python tools/bench_configs.py [--only cfg2,cfg5] [--steps 5]
@@ -100,6 +100,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="cfg1,cfg2,cfg3,cfg4,cfg5")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--cfg5-pool", type=int, default=200,
+                    help="resident client rows config 5 streams from (200 x 500 MB = 100 GB; "
+                         "each extra pass costs 8P bytes of accumulator traffic)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -157,17 +160,17 @@ def main():
         torch.cuda.empty_cache()
 
     if "cfg5" in only:
-        K, P, pool = 12_500, 125_000_000, 100
-        passes = K // pool
+        K, P, pool = 12_500, 125_000_000, a.cfg5_pool
+        counts = [min(pool, K - k0) for k0 in range(0, K, pool)]  # the last pass may be short
         Xb = blocked_random(pool, P, dev, 3 + rank)
         ws = [int(v) for v in rng.integers(50, 601, size=pool)]
         w32 = torch.tensor([ops.fl32(v) for v in ws], device=dev)
-        W_total = sum(ws) * passes * world
+        W_total = sum(sum(ws[:n]) for n in counts) * world
         acc = torch.empty(P, device=dev)
 
         def fn():
-            for i in range(passes):
-                ops.reduce_blocked(Xb, w32, acc, acc_in=None if i == 0 else acc,
+            for i, n in enumerate(counts):
+                ops.reduce_blocked(Xb, w32, acc, B=n, acc_in=None if i == 0 else acc,
                                    flags=ops.default_flags(Xb.shape[2]))
             if dist is not None:
                 dist.all_reduce(acc)
@@ -176,8 +179,9 @@ def main():
         if dist is not None:
             dist.barrier()
         report("cfg5_client_shard_allreduce", K, P, timed(fn, max(1, a.steps // 2), warmup=1),
-               dict(pool_rows=pool, note="K_per_gpu streamed from a resident 50 GB pool; "
-                                         "RCCL all-reduce of 4P bytes when N>1"))
+               dict(pool_rows=pool, passes=len(counts),
+                    note=f"K_per_gpu streamed from a resident {pool * P * 4 / 1e9:.0f} GB pool; "
+                         "RCCL all-reduce of 4P bytes when N>1"))
         del Xb
 
     if rank == 0:
