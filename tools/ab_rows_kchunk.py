@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--no-slab", action="store_true")
+    ap.add_argument("--nt", type=int, default=0, help="1: non-temporal row loads (the product default)")
     a = ap.parse_args()
     K, P = a.K, a.P
     dev = torch.device("cuda:0")
@@ -44,6 +45,7 @@ def main():
     table = ops.row_table(rows, dev)
     out = torch.empty(P, device=dev)
     chunks = [int(c) for c in a.chunks.split(",") if int(c) > 0]
+    nt = ops.FEDAGG_NT if a.nt else 0
 
     def run_chunked(kc):
         k0 = 0
@@ -52,7 +54,7 @@ def main():
             last = k0 + n >= K
             ops.reduce_rows(rows[k0:k0 + n], w32[k0:k0 + n], out,
                             acc_in=None if k0 == 0 else out, W=W if last else None,
-                            table=table[k0:k0 + n], checked=True)
+                            table=table[k0:k0 + n], checked=True, flags=nt)
             k0 += n
 
     variants = [(f"kc{kc}", (lambda kc=kc: run_chunked(kc))) for kc in chunks]
@@ -62,7 +64,7 @@ def main():
         Xb = torch.empty(ops.blocked_shape(K, P, C), device=dev)
         for k in range(K):
             ops.pack_row(rows[k], Xb, k)
-        variants.append((f"slab_C{C}", lambda: ops.reduce_blocked(Xb, w32, out, W=W)))
+        variants.append((f"slab_C{C}", lambda: ops.reduce_blocked(Xb, w32, out, W=W, flags=nt)))
     torch.cuda.synchronize()
     times = {n: [] for n, _ in variants}
     ref = None
