@@ -296,12 +296,24 @@ __device__ __forceinline__ StepOut step_math(float a, float c, float x, float b,
 // Epilogues: what a kernel does with a finished column value (the average, or
 // the raw sum).  `off` is the column's byte offset in a [P] vector.
 // ---------------------------------------------------------------------------
+// Epilogue operands, read with the first row batch (k_reduce_narrow).
+template <class V>
+struct EpiOps {
+  V c, x, b;
+};
+
 struct EpiStore {  // plain reduce: store it
   float* out;
   template <class V>  // f32x4 / f32x2 columns at byte offset `off`
   __device__ __forceinline__ void vec(int64_t off, V a) const {
     *reinterpret_cast<V*>(reinterpret_cast<char*>(out) + off) = a;
   }
+  template <class V>
+  __device__ __forceinline__ EpiOps<V> load_ops(int64_t) const { return {}; }
+  template <class V>
+  __device__ __forceinline__ void pin(EpiOps<V>&) const {}
+  template <class V>
+  __device__ __forceinline__ void vec_with(int64_t off, V a, const EpiOps<V>&) const { vec(off, a); }
   __device__ __forceinline__ void one(int64_t col, float a) const { out[col] = a; }
 };
 
@@ -334,16 +346,36 @@ struct EpiStep {  // server step on the average, in registers
     if constexpr (MOM) p.buf[i] = o.buf;
     p.cloud[i] = o.cloud;
   }
+  template <class V>  // the step's operands of the columns at byte offset `off`
+  __device__ __forceinline__ EpiOps<V> load_ops(int64_t off) const {
+    auto at = [off](float* q) {
+      return reinterpret_cast<const V*>(reinterpret_cast<const char*>(q) + off);
+    };
+    EpiOps<V> o{};
+    o.c = *at(p.cloud);
+    if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) o.x = *at(p.aux);
+    if constexpr (MOM) o.b = *at(p.buf);
+    return o;
+  }
+  // keeps the compiler from sinking load_ops past the row loop: the values
+  // must be in VGPRs here (one wait, while the first row batch is in flight)
+  template <class V>
+  __device__ __forceinline__ void pin(EpiOps<V>& o) const {
+    asm volatile("" : "+v"(o.c));
+    if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) asm volatile("" : "+v"(o.x));
+    if constexpr (MOM) asm volatile("" : "+v"(o.b));
+  }
   template <class V>  // f32x4 / f32x2 columns at byte offset `off`
   __device__ __forceinline__ void vec(int64_t off, V a) const {
+    vec_with(off, a, load_ops<V>(off));
+  }
+  template <class V>
+  __device__ __forceinline__ void vec_with(int64_t off, V a, const EpiOps<V>& o) const {
     constexpr int N = sizeof(V) / sizeof(float);
     auto at = [off](float* q) {
       return reinterpret_cast<V*>(reinterpret_cast<char*>(q) + off);
     };
-    const V c = *at(p.cloud);
-    V x = {}, b = {};
-    if constexpr (ALGO != FEDAGG_ALGO_FEDAVG) x = *at(p.aux);
-    if constexpr (MOM) b = *at(p.buf);
+    const V c = o.c, x = o.x, b = o.b;
     V nc, g, nx, nb;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
@@ -658,6 +690,9 @@ struct NarrowStrided {
   }  FEDAGG_NO_ROW_PREFETCH
 };
 
+template <int VW> struct EpiVec { using type = f32x4; };
+template <> struct EpiVec<2> { using type = f32x2; };
+
 template <int U, int VW, bool NT, class NR, class Epi>
 __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const float* __restrict__ w,
                                                           int64_t B, int64_t P,
@@ -671,6 +706,14 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
 #pragma unroll
   for (int e = 0; e < VW; ++e) a[e] = (flags & FEDAGG_INIT) ? 0.f : acc_in[c + e];
   int64_t k = 0;
+  // The step's operands (cloud / aux / momentum buffer) are read with the
+  // first row batch, not after the last one: a wave that ends in a dependent
+  // load keeps its slot from streaming rows for a memory latency (+0.5 % at
+  // 1000 x 25 M, +0.5..1.1 % at 1..8 M columns; profiles/r01bw/).
+  using EV = typename EpiVec<VW>::type;
+  EpiOps<EV> pre{};
+  if constexpr (VW >= 2) pre = epi.template load_ops<EV>(c * 4);
+  bool pinned = false;
   // row addresses of the next batch are fetched while this batch streams
   // (clamped to the last full batch, so the table is never over-read)
   decltype(rows.template prefetch<U>(0)) next{};
@@ -681,6 +724,12 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = rows.template load_at<VW, NT, U>(cur, k, u, voff);
     next = rows.template prefetch<U>(k + 2 * U <= B ? k + U : k);
+    if constexpr (VW >= 2) {
+      if (!pinned) {
+        epi.pin(pre);
+        pinned = true;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float wk = w[k + u];
@@ -713,9 +762,9 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
   }
   if (ok) {
     if constexpr (VW == 4) {
-      epi.vec(c0 * 4, f32x4{a[0], a[1], a[2], a[3]});
+      epi.vec_with(c0 * 4, f32x4{a[0], a[1], a[2], a[3]}, pre);
     } else if constexpr (VW == 2) {
-      epi.vec(c0 * 4, f32x2{a[0], a[1]});
+      epi.vec_with(c0 * 4, f32x2{a[0], a[1]}, pre);
     } else {
       epi.one(c0, a[0]);
     }
