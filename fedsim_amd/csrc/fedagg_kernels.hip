@@ -693,26 +693,41 @@ struct NarrowStrided {
 template <int VW> struct EpiVec { using type = f32x4; };
 template <> struct EpiVec<2> { using type = f32x2; };
 
-template <int U, int VW, bool NT, class NR, class Epi>
+// PC pieces per lane: lane t owns columns c0 + j*64*VW .. +VW-1 for j < PC, so
+// one wave reads PC * 64 * VW * 4 contiguous bytes of each row per visit, as PC
+// separate VW-wide loads (PC = 2 for borrowed rows, see the dispatch; the
+// column-blocked slab keeps PC = 1, its workgroup span must stay in a block).
+template <int U, int VW, bool NT, class NR, class Epi, int PC = 1>
 __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const float* __restrict__ w,
                                                           int64_t B, int64_t P,
                                                           const float* acc_in, Epi epi,
                                                           float W32, int flags) {
-  const int64_t c0 = (static_cast<int64_t>(blockIdx.x) * kNarrowBlock + threadIdx.x) * VW;
-  const bool ok = c0 < P;
-  const int64_t c = ok ? c0 : P - VW;  // clamp: load something valid, store nothing
-  const uint32_t voff = rows.template lane_off<VW>(c);
-  float a[VW];
+  constexpr int64_t kPiece = int64_t(kNarrowBlock) * VW;  // columns of one piece
+  const int64_t cb = static_cast<int64_t>(blockIdx.x) * kPiece * PC + threadIdx.x * VW;
+  int64_t c0[PC], c[PC];
+  bool ok[PC];
+  uint32_t voff[PC];
+  float a[PC][VW];
 #pragma unroll
-  for (int e = 0; e < VW; ++e) a[e] = (flags & FEDAGG_INIT) ? 0.f : acc_in[c + e];
+  for (int j = 0; j < PC; ++j) {
+    c0[j] = cb + j * kPiece;
+    ok[j] = c0[j] < P;
+    c[j] = ok[j] ? c0[j] : P - VW;  // clamp: load something valid, store nothing
+    voff[j] = rows.template lane_off<VW>(c[j]);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) a[j][e] = (flags & FEDAGG_INIT) ? 0.f : acc_in[c[j] + e];
+  }
   int64_t k = 0;
   // The step's operands (cloud / aux / momentum buffer) are read with the
   // first row batch, not after the last one: a wave that ends in a dependent
   // load keeps its slot from streaming rows for a memory latency (+0.5 % at
   // 1000 x 25 M, +0.5..1.1 % at 1..8 M columns; profiles/r01bw/).
   using EV = typename EpiVec<VW>::type;
-  EpiOps<EV> pre{};
-  if constexpr (VW >= 2) pre = epi.template load_ops<EV>(c * 4);
+  EpiOps<EV> pre[PC]{};
+  if constexpr (VW >= 2) {
+#pragma unroll
+    for (int j = 0; j < PC; ++j) pre[j] = epi.template load_ops<EV>(c[j] * 4);
+  }
   bool pinned = false;
   // row addresses of the next batch are fetched while this batch streams
   // (clamped to the last full batch, so the table is never over-read)
@@ -720,13 +735,16 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
   if (U <= B) next = rows.template prefetch<U>(0);
   for (; k + U <= B; k += U) {
     const auto cur = next;
-    Cols<VW> v[U];
+    Cols<VW> v[U][PC];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = rows.template load_at<VW, NT, U>(cur, k, u, voff);
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < PC; ++j) v[u][j] = rows.template load_at<VW, NT, U>(cur, k, u, voff[j]);
     next = rows.template prefetch<U>(k + 2 * U <= B ? k + U : k);
     if constexpr (VW >= 2) {
       if (!pinned) {
-        epi.pin(pre);
+#pragma unroll
+        for (int j = 0; j < PC; ++j) epi.pin(pre[j]);
         pinned = true;
       }
     }
@@ -734,7 +752,9 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
     for (int u = 0; u < U; ++u) {
       const float wk = w[k + u];
 #pragma unroll
-      for (int e = 0; e < VW; ++e) a[e] = axpy_rn(a[e], v[u].v[e], wk);
+      for (int j = 0; j < PC; ++j)
+#pragma unroll
+        for (int e = 0; e < VW; ++e) a[j][e] = axpy_rn(a[j][e], v[u][j].v[e], wk);
     }
   }
   if (k < B) {
@@ -743,30 +763,40 @@ __global__ __launch_bounds__(kNarrowBlock) void k_reduce_narrow(NR rows, const f
     // made of); issue them all before the in-order adds, under wave-uniform
     // guards
     const int64_t rem = B - k;
-    Cols<VW> v[U - 1];
+    Cols<VW> v[U - 1][PC];
 #pragma unroll
     for (int u = 0; u < U - 1; ++u)
-      if (u < rem) v[u] = rows.template load<VW, NT>(k + u, voff);
+      if (u < rem) {
+#pragma unroll
+        for (int j = 0; j < PC; ++j) v[u][j] = rows.template load<VW, NT>(k + u, voff[j]);
+      }
 #pragma unroll
     for (int u = 0; u < U - 1; ++u) {
       if (u < rem) {
         const float wk = w[k + u];
 #pragma unroll
-        for (int e = 0; e < VW; ++e) a[e] = axpy_rn(a[e], v[u].v[e], wk);
+        for (int j = 0; j < PC; ++j)
+#pragma unroll
+          for (int e = 0; e < VW; ++e) a[j][e] = axpy_rn(a[j][e], v[u][j].v[e], wk);
       }
     }
   }
   if (flags & FEDAGG_FINALIZE) {
 #pragma unroll
-    for (int e = 0; e < VW; ++e) a[e] = a[e] / W32;
+    for (int j = 0; j < PC; ++j)
+#pragma unroll
+      for (int e = 0; e < VW; ++e) a[j][e] = a[j][e] / W32;
   }
-  if (ok) {
-    if constexpr (VW == 4) {
-      epi.vec_with(c0 * 4, f32x4{a[0], a[1], a[2], a[3]}, pre);
-    } else if constexpr (VW == 2) {
-      epi.vec_with(c0 * 4, f32x2{a[0], a[1]}, pre);
-    } else {
-      epi.one(c0, a[0]);
+#pragma unroll
+  for (int j = 0; j < PC; ++j) {
+    if (ok[j]) {
+      if constexpr (VW == 4) {
+        epi.vec_with(c0[j] * 4, f32x4{a[j][0], a[j][1], a[j][2], a[j][3]}, pre[j]);
+      } else if constexpr (VW == 2) {
+        epi.vec_with(c0[j] * 4, f32x2{a[j][0], a[j][1]}, pre[j]);
+      } else {
+        epi.one(c0[j], a[j][0]);
+      }
     }
   }
 }
@@ -1114,10 +1144,37 @@ int max_cols_per_lane(int64_t P, std::initializer_list<const void*> ptrs) {
   return v;
 }
 
+// Borrowed rows (pointer table) with two columns per lane read two pieces per
+// lane from P >= kRowsPiecesP on, with at most kRowsPiecesU rows in flight
+// (build knobs for the A/B in tools/ab_rows_variants.py).
+#ifndef FEDAGG_ROWS_PC
+#define FEDAGG_ROWS_PC 2
+#endif
+#ifndef FEDAGG_ROWS_PCU
+#define FEDAGG_ROWS_PCU 8
+#endif
+#ifndef FEDAGG_ROWS_PC_LOG2P
+#define FEDAGG_ROWS_PC_LOG2P 22
+#endif
+constexpr int kRowsPieces = FEDAGG_ROWS_PC;
+constexpr int kRowsPiecesU = FEDAGG_ROWS_PCU;
+constexpr int64_t kRowsPiecesP = int64_t(1) << FEDAGG_ROWS_PC_LOG2P;
+
 template <int U, int VW, bool NT, class NR, class Epi>
 hipError_t launch_narrow_t(const NR& rows, const float* w, int64_t B, int64_t P,
                            const float* acc_in, const Epi& epi, float W32, int flags,
                            hipStream_t s) {
+  if constexpr (std::is_same_v<NR, NarrowTable> && VW == 2 && kRowsPieces > 1) {
+    if (P >= kRowsPiecesP) {
+      constexpr int UP = U < kRowsPiecesU ? U : kRowsPiecesU;
+      constexpr int64_t span = int64_t(kNarrowBlock) * VW * kRowsPieces;
+      const int64_t g = (P + span - 1) / span;
+      hipLaunchKernelGGL((k_reduce_narrow<UP, VW, NT, NR, Epi, kRowsPieces>),
+                         dim3(static_cast<unsigned>(g)), dim3(kNarrowBlock), 0, s, rows, w, B, P,
+                         acc_in, epi, W32, flags);
+      return hipGetLastError();
+    }
+  }
   const int64_t grid = (P + kNarrowBlock * VW - 1) / (kNarrowBlock * VW);
   hipLaunchKernelGGL((k_reduce_narrow<U, VW, NT, NR, Epi>), dim3(static_cast<unsigned>(grid)),
                      dim3(kNarrowBlock), 0, s, rows, w, B, P, acc_in, epi, W32, flags);

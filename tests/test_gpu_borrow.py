@@ -253,3 +253,29 @@ def test_pop_step_split_policy_bitwise(borrow, algo, dev):
         avg = ref.reduce(X, w, W=sum(w))
         np.testing.assert_array_equal(bits(outs[0][0]),
                                       bits(ref.fedavg_sgd(avg, cloud0.cpu().numpy(), 0.3)))
+
+
+@pytest.mark.parametrize("K", [3, 21])
+@pytest.mark.parametrize("P", [(1 << 22) + 130, (1 << 22) + 256 + 2, 1 << 22])
+def test_borrowed_rows_two_pieces_bitwise(K, P, dev):
+    """From P = 2^22 on, borrowed rows take the two-pieces-per-lane kernel (a
+    wave reads 1 KiB of each row per visit): ragged last wave (second piece
+    past P, or both pieces partial), fewer rows than one unrolled batch, and a
+    batch tail. Plain reduce and fused FedAvg step vs the oracle, bitwise."""
+    from fedsim_amd import ops
+
+    X = V.client_rows("normal", K, P, 31)
+    w = V.client_weights("fedavg", K, 31)
+    rows = [torch.from_numpy(X[k].copy()).to(dev) for k in range(K)]
+    w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
+    out = torch.full((P,), float("nan"), device=dev)
+    ops.reduce_rows(rows, w32, out, W=sum(w))
+    avg = ref.reduce(X, w, W=sum(w))
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(avg))
+    cloud0 = V.cloud_vector(P, 32)
+    cloud = torch.from_numpy(cloud0.copy()).to(dev)
+    grad = torch.empty_like(cloud)
+    ops.reduce_rows_step(rows, w32, ops.ServerStep("fedavg", cloud, lr=0.3, grad_out=grad),
+                         W=sum(w))
+    np.testing.assert_array_equal(bits(cloud.cpu().numpy()),
+                                  bits(ref.fedavg_sgd(avg, cloud0, 0.3)))
