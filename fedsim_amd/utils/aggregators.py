@@ -374,7 +374,7 @@ class _DeviceEntry(object):
         else:
             fusable = self.n_pending > 0 and ops.can_fuse_step(self.slab, step)
             rows = self.n_pending
-        if not fusable or not ops.fuse_step_pays(self.P, rows):
+        if not fusable or not ops.fuse_step_pays(self.P, rows, borrowed=bool(self.borrowed)):
             step.apply(self.pop(on_device=True).reshape(-1))
             return
         self._flush(final_W=self.cur_w if self._weighted() else None, step=step)

@@ -155,7 +155,8 @@ def test_build_is_gfx950():
 
 def test_fuse_step_policy():
     """ops.fuse_step_pays: the last drain runs the server step fused except at
-    2^20 <= P < 2^24 with >= 128 rows (profiles/r01bq/, r01br/, r01bs/)."""
+    2^20 <= P < 2^24 with >= 128 rows (profiles/r01bq/, r01br/, r01bs/), and
+    for borrowed rows at any P >= 2^20 with >= 128 rows (r01cf/)."""
     from fedsim_amd import ops
 
     assert ops.fuse_step_pays(25_000_000, 1000)       # headline: fused
@@ -165,6 +166,11 @@ def test_fuse_step_policy():
     assert not ops.fuse_step_pays(1_085_668, 128)     # SimpleCNN2 x 1000 clients: split
     assert not ops.fuse_step_pays((1 << 24) - 1, 1000)
     assert ops.fuse_step_pays(1 << 24, 1000)
+    # borrowed rows (pointer table): split from 2^20 columns on, any size
+    assert not ops.fuse_step_pays(25_000_000, 1000, borrowed=True)
+    assert not ops.fuse_step_pays(1 << 20, 128, borrowed=True)
+    assert ops.fuse_step_pays(25_000_000, 127, borrowed=True)
+    assert ops.fuse_step_pays(199_210, 1000, borrowed=True)
 
 
 def test_column_mapping_decision():

@@ -145,9 +145,10 @@ def test_borrowed_pop_step_matches_two_step(algo, momentum, dev):
 def test_borrowed_full_size_round(dev):
     """Headline size through the borrowing aggregator: 1000 separate HBM
     client tensors of 25 M floats (100 GB).  The default HBM budget makes the
-    aggregator drain once in the middle (accumulator chaining) and fuse the
-    FedAvg step into the last drain; the result equals one pass of the
-    row-pointer kernel bitwise, and the oracle on 4096 sampled columns."""
+    aggregator drain once in the middle (accumulator chaining) and run the
+    FedAvg step after the last drain (split, ops.fuse_step_pays); the result
+    equals one fused pass of the row-pointer kernel bitwise, and the oracle on
+    4096 sampled columns."""
     from fedsim_amd import ops
     from fedsim_amd.utils import SerialAggregator
 
