@@ -34,6 +34,12 @@
 //     block's workgroups stream one contiguous region.  Those loads go through
 //     one buffer descriptor per workgroup with the row in an SGPR soffset:
 //     buffer_load_dword{,x2,x4} v, v_off, s[rsrc], s_row offen nt.
+//   * Client tensors the caller keeps in HBM ("borrowed" rows, a device table
+//     of row pointers) are read where they lie; from 2^22 columns on a lane
+//     there owns two pieces of 128 columns, so a wave reads 1 KiB of each row
+//     per visit as two 512-byte loads (k_reduce_narrow<..., PC = 2>).
+//   * A fused server step reads its operands (cloud / aux / momentum buffer)
+//     with the first row batch, so no wave ends waiting on a dependent load.
 //   * Layout / mapping / unroll / nt were chosen by measurement
 //     (tools/sweep_reduce.py, tools/sweep_mapping.py, tools/ab_mapping.py,
 //     profiles/).
