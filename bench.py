@@ -1,53 +1,75 @@
 """Benchmark: client-update bytes/s reduced (device-resident), K clients x P params.
 
-One step = one FedAvg server round on the MI355X, device-resident: the
-weighted exact-mode reduction of K client rows, the pop divide and the FedAvg
-server SGD step (pseudo-gradient stored as cloud.grad) in ONE pass over the
-slab (fedagg_reduce_step_blocked_f32) -- what SerialAggregator.add x K +
+One step = one FedAvg server round on the MI355X, device-resident: the exact
+weighted reduction of K client rows, the pop divide and the FedAvg server SGD
+step (pseudo-gradient stored as cloud.grad) -- what SerialAggregator.add x K +
 FedAvg.optimize does in this package.  Reference: SerialAggregator.add / pop
 (fedsim/utils/aggregators.py:23-122) + FedAvg.optimize
 (fedsim/distributed/centralized/training/fedavg.py:193-208), with the client
-vectors already packed in HBM.  --step split times the two-launch variant
-(reduce + divide, then the epilogue kernel).
+vectors already packed in HBM.
 
-Multi-GPU (launched by torch.distributed.run): parameter-sharded weak scaling,
-SURVEY §8e — rank g owns a contiguous P-column shard of an N*P-parameter model
-and reduces all K clients over it; no data-path collective (a barrier and a
-max-over-ranks of the elapsed time only).  value = 4*K*P*N / max_time.
+Modes (``--mode``), one process per GPU, SURVEY §8e:
 
-Prints ONE JSON line on rank 0.
+* ``param`` (default; the headline, BASELINE configs[1]'s K=1000 x P=25 M per
+  GPU): weak scaling.  Rank g owns a contiguous 25 M-column shard of an
+  N*25 M-parameter model and runs the round over all K clients on it: ONE
+  launch of fedagg_reduce_step_blocked_f32 (reduce + divide + server step in
+  one pass).  No data-path collective.  value = 4*K*P*N / max-over-ranks time.
+* ``strong`` (config 4): FedAvg 10 000 clients x 25 M params in total,
+  parameter-sharded over N GPUs (64-aligned column shards, no collective).  A
+  shard that does not fit HBM (N <= 2) streams from a resident pool of
+  distinct client rows, chained through the accumulator (declared in the line).
+* ``allreduce`` (config 5): client-sharded, 12 500 clients x 125 M params per
+  GPU (x8 = 100 000), streamed from a resident 200-row pool, then ONE RCCL
+  all-reduce(sum) of the 4P-byte partial over xGMI, the divide by fl32(W) and
+  the server step.  The all-reduce's share of the round is reported
+  separately.  Reordered sum: normwise parity.
+
+Launch: ``python bench.py --gpus N`` spawns N rank processes itself (before
+anything touches a GPU) when it is not already running under
+torch.distributed.run; either way rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from fedsim_amd import ops  # noqa: E402
-
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "client-update bytes/s reduced (device-resident), K clients × P params"
+# per-mode workload defaults: (K, P, K means) -- BASELINE.json configs 1, 4, 5
+MODE_DEFAULTS = {
+    "param": (1000, 25_000_000, "clients per round; P per GPU shard"),
+    "strong": (10_000, 25_000_000, "clients per round; P = whole model, sharded over N"),
+    "allreduce": (12_500, 125_000_000, "clients per GPU (x N in total); P = whole model"),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--K", type=int, default=1000, help="clients per round")
-    ap.add_argument("--P", type=int, default=25_000_000, help="params per GPU shard")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed rounds (default 20; 5 for strong, 3 for allreduce)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed rounds (default 3; 1 for strong / allreduce)")
+    ap.add_argument("--mode", default="param", choices=sorted(MODE_DEFAULTS))
+    ap.add_argument("--K", type=int, default=None, help="clients (see --mode)")
+    ap.add_argument("--P", type=int, default=None, help="params (see --mode)")
+    ap.add_argument("--pool-rows", type=int, default=None,
+                    help="resident client rows the streamed modes re-read (allreduce: 200; "
+                         "strong: as many as fit)")
     ap.add_argument("--layout", default="blocked", choices=["blocked", "strided"],
-                    help="HBM slab layout (blocked: column blocks of C floats, rows "
-                         "contiguous inside a block; strided: row-major [K, ldx])")
+                    help="param mode's HBM slab layout (blocked: column blocks of C floats, "
+                         "rows contiguous inside a block; strided: row-major [K, ldx])")
     ap.add_argument("--C", type=int, default=4096, choices=[1024, 2048, 4096])
     ap.add_argument("--unroll", type=int, default=4, choices=[0, 2, 4, 8, 16])
     ap.add_argument("--vpt", type=int, default=2, choices=[0, 1, 2, 4],
@@ -63,115 +85,88 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--master-port", type=int, default=0,
+                    help="rendezvous port of the self-spawned ranks (0: pick a free one)")
+    ap.add_argument("--rehearsal-stub", default=None, metavar="MODULE:FN",
+                    help="TEST ONLY: run the launcher and the collectives on CPU over gloo, "
+                         "with the per-rank reduction done by MODULE:FN (no GPU, no HIP "
+                         "kernel; the line is marked as a rehearsal and carries no roofline)")
+    a = ap.parse_args(argv)
+    K, P, _ = MODE_DEFAULTS[a.mode]
+    a.K = K if a.K is None else a.K
+    a.P = P if a.P is None else a.P
+    heavy = a.mode != "param"
+    a.steps = (3 if a.mode == "allreduce" else 5 if heavy else 20) if a.steps is None else a.steps
+    a.warmup = (1 if heavy else 3) if a.warmup is None else a.warmup
+    return a
 
 
-def dist_setup():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    pg = None
-    # any torch.distributed.run launch (even --nproc-per-node 1) takes the
-    # process-group path, so the N=1 rehearsal exercises the same barrier /
-    # max-over-ranks code the N>1 runs use
-    if world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ):
-        import torch.distributed as dist
-
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-        pg = dist
-    return world, rank, local, pg
+# --------------------------------------------------------------------------
+# launcher: N rank processes from a parent that never touches the GPU
+# --------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def make_inputs(K, P, rank, dev, layout, C):
-    """x_k = base + eps_k, base ~ N(0, 0.05) (seed 7), eps_k ~ N(0, 1e-3)
-    (Philox, seed 20261015 + row block); FedAvg weights w_k ~ U{50..600}
-    (numpy seed 11).
-
-    strided: row-major [K, ldx] fp32 slab, 256-B aligned rows.
-    blocked: [ceil(P/C), K, C] — column block b holds rows 0..K-1 of columns
-             [bC, bC+C) contiguously (include/fedagg.h), the layout the
-             aggregator packs client vectors into."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(7 + 1_000_003 * rank)
-    base = torch.empty(P, dtype=torch.float32, device=dev).normal_(0.0, 0.05, generator=g)
-    blk = 64
-    if layout == "strided":
-        ldx = (P + 63) // 64 * 64
-        X = torch.empty((K, ldx), dtype=torch.float32, device=dev)
-    else:
-        X = torch.zeros(ops.blocked_shape(K, P, C), dtype=torch.float32, device=dev)
-        tmp = torch.empty((blk, P), dtype=torch.float32, device=dev)
-        full = P // C
-    for k0 in range(0, K, blk):
-        k1 = min(K, k0 + blk)
-        g.manual_seed(20261015 + k0 + 1_000_003 * rank)
-        if layout == "strided":
-            X[k0:k1, :P].normal_(0.0, 1e-3, generator=g).add_(base)
-        else:
-            t = tmp[: k1 - k0].normal_(0.0, 1e-3, generator=g).add_(base)
-            X[:full, k0:k1, :].copy_(t[:, : full * C].view(k1 - k0, full, C).transpose(0, 1))
-            if P % C:
-                X[full, k0:k1, : P % C].copy_(t[:, full * C:])
-    del base
-    weights = [int(v) for v in np.random.default_rng(11).integers(50, 601, size=K)]
-    return X, weights
-
-
-def load_pmc(path, K, P, kernel, layout, step):
-    """HBM bytes per launch from the committed PMC summary
-    (tools/pmc_traffic.py), when it was measured on this exact kernel and
-    workload; else None."""
+def launch(a, argv):
+    """Start ranks 0..N-1 of this script (one per GPU) as child processes with
+    the torch.distributed.run environment, relay rank 0's result line, and
+    return the worst exit code.  The parent imports neither torch's HIP runtime
+    nor libfedagg, so nothing is initialised on a GPU before the children
+    start; a rank that fails ends the others."""
+    n = a.gpus
+    port = a.master_port or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), FEDSIM_BENCH_CHILD="1")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.abspath(__file__), *argv], env=env,
+            stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    out = []
+    rc = 0
     try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if d.get("K") == K and d.get("P") == P and d.get("kernel") == kernel and \
-            d.get("layout", "strided") == layout and d.get("step", "split") == step:
-        return d.get("hbm_bytes_per_launch")
-    return None
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        out = procs[0].stdout.read().splitlines()
+    lines = [ln for ln in out if ln.startswith("{")]
+    if rc == 0 and len(lines) != 1:
+        sys.stderr.write("bench: rank 0 printed %d result lines\n" % len(lines))
+        rc = 1
+    for ln in out:
+        if not ln.startswith("{"):
+            sys.stderr.write(ln + "\n")
+    if lines:
+        print(lines[-1], flush=True)
+    return rc
 
 
-def cpu_baseline(P, budget_s):
-    """The reference's per-client loop restated on torch CPU (oracle leg),
-    timed on a bounded sample of the same workload: distinct client tensors of
-    the headline P, as many clients as fit ~budget_s of host time."""
-    from oracle.reference_loop import aggregate_round
-
-    threads = torch.get_num_threads()
-    rng = np.random.default_rng(11)
-    pool_n = 8
-    pool = [torch.randn(P) for _ in range(pool_n)]
-    weights = [int(v) for v in rng.integers(50, 601, size=4096)]
-    t0 = time.perf_counter()
-    aggregate_round(pool[:2], weights[:2])
-    per_client = (time.perf_counter() - t0) / 2
-    n = int(max(4, min(2000, budget_s / max(per_client, 1e-6))))
-    rows = [pool[k % pool_n] for k in range(n)]
-    t0 = time.perf_counter()
-    aggregate_round(rows, weights[:n])
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        cpu = platform.processor()
-    return dict(
-        value=4.0 * n * P / dt / 1e9,
-        unit="GB/s",
-        cores=threads,
-        kind="port",
-        sample=(f"oracle/reference_loop.aggregate_round (torch CPU clone + mul + add per client, "
-                f"then divide) over {n} clients x P={P} fp32 (pool of {pool_n} distinct host "
-                f"tensors), {dt:.2f} s on {threads} threads of {cpu}"),
-    )
-
-
+# --------------------------------------------------------------------------
+# ranks
+# --------------------------------------------------------------------------
 class _StdoutToStderr(object):
     """Route file descriptor 1 to stderr until the result line is printed,
     so that banners written by native libraries (RCCL prints its version
@@ -198,33 +193,263 @@ class _StdoutToStderr(object):
         self.saved = None
 
 
-def main():
-    quiet = _StdoutToStderr()
+class Rank(object):
+    """This process's place in the job and its device plumbing."""
+
+    def __init__(self, a):
+        import torch
+
+        self.torch = torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.rehearsal = a.rehearsal_stub is not None
+        self.dist = None
+        if self.rehearsal:
+            mod, fn = a.rehearsal_stub.split(":")
+            self.stub = getattr(importlib.import_module(mod), fn)
+            self.dev = torch.device("cpu")
+        else:
+            torch.cuda.set_device(self.local)
+            self.dev = torch.device("cuda", self.local)
+        # any torch.distributed.run launch (even --nproc-per-node 1) takes the
+        # process-group path, so the N=1 rehearsal exercises the same barrier /
+        # max-over-ranks code the N>1 runs use
+        if self.world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ):
+            import torch.distributed as dist
+
+            if self.rehearsal:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group(backend="nccl", device_id=self.dev)
+            self.dist = dist
+
+    def sync(self):
+        if not self.rehearsal:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, *vals):
+        if self.dist is None:
+            return vals
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return tuple(float(v) for v in t.tolist())
+
+
+class KernelClock(object):
+    """Per-launch HIP events on the stream the library launches on (the
+    current torch stream), so ``achieved`` is algorithmic bytes over kernel
+    time, not over the round's wall clock."""
+
+    def __init__(self, rk):
+        self.rk = rk
+        self.marks = []  # (bytes, ev0, ev1)
+        self.on = False
+
+    def run(self, nbytes, fn):
+        if not self.on or self.rk.rehearsal:
+            return fn()
+        torch = self.rk.torch
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn()
+        e1.record()
+        self.marks.append((nbytes, e0, e1))
+        return r
+
+    def summary(self):
+        """(algorithmic bytes per launch, mean launch ms)."""
+        if not self.marks:
+            return None, None
+        ms = [e0.elapsed_time(e1) for _, e0, e1 in self.marks]
+        nb = sum(b for b, _, _ in self.marks)
+        return nb / len(self.marks), sum(ms) / len(ms)
+
+
+def _weights(K, seed=11):
+    import numpy as np
+
+    return [int(v) for v in np.random.default_rng(seed).integers(50, 601, size=K)]
+
+
+def make_inputs(rk, K, P, layout, C):
+    """x_k = base + eps_k, base ~ N(0, 0.05) (seed 7), eps_k ~ N(0, 1e-3)
+    (Philox, seed 20261015 + row block); FedAvg weights w_k ~ U{50..600}
+    (numpy seed 11).
+
+    strided: row-major [K, ldx] fp32 slab, 256-B aligned rows.
+    blocked: [ceil(P/C), K, C] -- column block b holds rows 0..K-1 of columns
+             [bC, bC+C) contiguously (include/fedagg.h), the layout the
+             aggregator packs client vectors into."""
+    from fedsim_amd import ops
+
+    torch, dev, rank = rk.torch, rk.dev, rk.rank
+    g = torch.Generator(device=dev)
+    g.manual_seed(7 + 1_000_003 * rank)
+    base = torch.empty(P, dtype=torch.float32, device=dev).normal_(0.0, 0.05, generator=g)
+    blk = 64
+    if layout == "strided" or rk.rehearsal:
+        ldx = (P + 63) // 64 * 64
+        X = torch.empty((K, ldx), dtype=torch.float32, device=dev)
+    else:
+        X = torch.zeros(ops.blocked_shape(K, P, C), dtype=torch.float32, device=dev)
+        tmp = torch.empty((blk, P), dtype=torch.float32, device=dev)
+        full = P // C
+    for k0 in range(0, K, blk):
+        k1 = min(K, k0 + blk)
+        g.manual_seed(20261015 + k0 + 1_000_003 * rank)
+        if layout == "strided" or rk.rehearsal:
+            X[k0:k1, :P].normal_(0.0, 1e-3, generator=g).add_(base)
+        else:
+            t = tmp[: k1 - k0].normal_(0.0, 1e-3, generator=g).add_(base)
+            X[:full, k0:k1, :].copy_(t[:, : full * C].view(k1 - k0, full, C).transpose(0, 1))
+            if P % C:
+                X[full, k0:k1, : P % C].copy_(t[:, full * C:])
+    return X
+
+
+def make_pool(rk, R, P, C, seed):
+    """A resident pool of R distinct client rows, column-blocked [ceil(P/C),
+    R, C], values N(0, 0.05) (Philox ``seed``): the streamed modes re-read it
+    cyclically to stand for K >> R clients (footprint >> the 256 MB MALL)."""
+    from fedsim_amd import ops
+
+    torch = rk.torch
+    g = torch.Generator(device=rk.dev).manual_seed(seed)
+    if rk.rehearsal:
+        return torch.empty((R, P)).normal_(0.0, 0.05, generator=g)
+    Xb = torch.empty(ops.blocked_shape(R, P, C), dtype=torch.float32, device=rk.dev)
+    for b0 in range(0, Xb.shape[0], 256):
+        Xb[b0:b0 + 256].normal_(0.0, 0.05, generator=g)
+    return Xb
+
+
+def load_pmc(path, K, P, kernel, layout, step):
+    """HBM bytes per launch from the committed PMC summary
+    (tools/pmc_traffic.py), when it was measured on this exact kernel and
+    workload; else None."""
     try:
-        _main(quiet)
-    finally:
-        quiet.restore()
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("K") == K and d.get("P") == P and d.get("kernel") == kernel and \
+            d.get("layout", "strided") == layout and d.get("step", "split") == step:
+        return d.get("hbm_bytes_per_launch")
+    return None
 
 
-def _main(quiet):
-    a = parse()
-    world, rank, local, dist = dist_setup()
-    dev = torch.device("cuda", local)
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: every CPU this process may run on,
+    capped by OMP_NUM_THREADS when the box sets it (the GPU pool sets it to
+    the box's CPU share, 16 per GPU: nproc there shows the whole machine).
+    Returns (threads, facts) -- facts go into the JSON line."""
+    affinity = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    try:
+        import psutil
+
+        physical = psutil.cpu_count(logical=False)
+    except Exception:  # noqa: BLE001 - optional fact
+        physical = None
+    return threads, dict(affinity_cpus=affinity, omp_num_threads=omp, physical_cores=physical,
+                         logical_cpus=os.cpu_count(), cpu_model=_cpu_model())
+
+
+def cpu_baseline(P, budget_s):
+    """The reference's per-client loop restated on torch CPU (oracle leg),
+    timed on a bounded sample of the same workload: distinct client tensors of
+    the workload's P, as many clients as fit ~budget_s of host time."""
+    import numpy as np
+    import torch
+
+    from oracle.reference_loop import aggregate_round
+
+    threads, facts = cpu_threads()
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(11)
+    pool_n = 8
+    pool = [torch.randn(P) for _ in range(pool_n)]
+    weights = [int(v) for v in rng.integers(50, 601, size=4096)]
+    t0 = time.perf_counter()
+    aggregate_round(pool[:2], weights[:2])
+    per_client = (time.perf_counter() - t0) / 2
+    n = int(max(4, min(2000, budget_s / max(per_client, 1e-6))))
+    rows = [pool[k % pool_n] for k in range(n)]
+    t0 = time.perf_counter()
+    aggregate_round(rows, weights[:n])
+    dt = time.perf_counter() - t0
+    return dict(
+        value=4.0 * n * P / dt / 1e9,
+        unit="GB/s",
+        cores=threads,
+        kind="port",
+        threads_rule="torch.set_num_threads(min(len(os.sched_getaffinity(0)), OMP_NUM_THREADS))",
+        **facts,
+        sample=(f"oracle/reference_loop.aggregate_round (torch CPU clone + mul + add per client, "
+                f"then divide) over {n} clients x P={P} fp32 (pool of {pool_n} distinct "
+                f"{4 * P / 1e6:.0f} MB host tensors, far above L3), {dt:.2f} s on {threads} "
+                f"threads of {facts['cpu_model']}"),
+    )
+
+
+def fedavg_step(rk, P):
+    """FedAvg.optimize's server step operands (default SGD lr 1.0,
+    fed_learn.py:129; cloud.grad = pseudo-gradient as torch leaves it)."""
+    from fedsim_amd import ops
+
+    torch = rk.torch
+    cloud = torch.zeros(P, dtype=torch.float32, device=rk.dev)
+    grad = torch.empty(P, dtype=torch.float32, device=rk.dev)
+    return ops.ServerStep("fedavg", cloud, lr=1.0, grad_out=grad), cloud, grad
+
+
+# -- param: the headline round ---------------------------------------------
+def setup_param(a, rk, clock):
+    from fedsim_amd import ops
+
+    torch = rk.torch
     K, P = a.K, a.P
+    X = make_inputs(rk, K, P, a.layout, a.C)
+    weights = _weights(K)
+    W = sum(weights)
+    w32 = torch.tensor([ops.fl32(v) for v in weights], dtype=torch.float32, device=rk.dev)
+    info = dict(clients_K=K, params_per_gpu_P=P, params_total=P * rk.world,
+                parallelism=f"param-shard{rk.world}" if rk.world > 1 else "single",
+                mode="exact (bitwise vs reference CPU)")
+    if rk.rehearsal:
+        out = torch.empty(P)
+        info["layout"] = "row-major (rehearsal)"
+
+        def step():
+            rk.stub(X[:, :P], w32, out, None, W)
+        return step, info, 4.0 * K * P * rk.world, (X,)
+
     flags = ops.tuning_flags(unroll=a.unroll, vpt=a.vpt if a.layout == "strided" else 0,
                              nt=bool(a.nt), mapping=a.mapping)
     fused = a.step == "fused" and a.layout == "blocked" and not a.no_epilogue
-    step_mode = "fused" if fused else "split"
-    X, weights = make_inputs(K, P, rank, dev, a.layout, a.C)
-    W = sum(weights)
-    w32 = torch.tensor([ops.fl32(v) for v in weights], dtype=torch.float32, device=dev)
-    avg = torch.empty(P, dtype=torch.float32, device=dev)
-    cloud = torch.zeros(P, dtype=torch.float32, device=dev)
-    grad = torch.empty(P, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    # FedAvg.optimize's server step (default SGD lr 1.0, fed_learn.py:129),
-    # cloud.grad = pseudo-gradient as torch leaves it
-    sstep = ops.ServerStep("fedavg", cloud, lr=1.0, grad_out=grad)
+    avg = torch.empty(P, dtype=torch.float32, device=rk.dev)
+    sstep, cloud, grad = fedavg_step(rk, P)
+    # client rows + weights, plus per column: fused = cloud read + cloud write +
+    # grad write; split (reduce kernel alone) = the average's write
+    nbytes = 4.0 * K * P + 4.0 * K + (12.0 * P if fused else 4.0 * P)
 
     def reduce():
         if fused:
@@ -234,102 +459,247 @@ def _main(quiet):
         else:
             ops.reduce_blocked(X, w32, avg, W=W, flags=flags)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        reduce()
-        if ev is not None:
-            ev[1].record(stream)
+    def step():
+        clock.run(nbytes, reduce)
         if not a.no_epilogue and not fused:
             ops.fedavg_sgd(avg, cloud, 1.0, grad_out=grad)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(a.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    total_bytes = 4.0 * K * P * world
-    value = total_bytes * a.steps / elapsed / 1e9
-    # client rows + weights, plus per column: fused = cloud read + cloud write +
-    # grad write; split (reduce kernel alone) = the average's write
-    alg_bytes_launch = 4.0 * K * P + 4.0 * K + (12.0 * P if fused else 4.0 * P)
-    achieved = alg_bytes_launch / (kern_ms * 1e-3) / 1e9
-    # the kernel the library launched: the fused step path takes only the
-    # mapping bits, the plain reduce all of `flags`
     mapping, unroll = ops.column_mapping(
         P, ops.tuning_flags(mapping=a.mapping) if fused else flags, B=K)
     kernel = ("k_reduce_vec" if mapping == "wide" else
               f"k_reduce_narrow<U={unroll}, VW={mapping[-1]}>")
-    traffic = load_pmc(a.pmc_json, K, P, kernel,
-                       a.layout if a.layout == "strided" else f"blocked{a.C}", step_mode)
+    step_mode = "fused" if fused else "split"
+    info.update(
+        workload=("FedAvg server round, device-resident: exact weighted reduce + divide "
+                  "+ SGD server step in one pass" if fused else
+                  "FedAvg server round, device-resident: exact weighted reduce + divide, "
+                  "then the SGD epilogue kernel"),
+        step=step_mode,
+        layout=a.layout if a.layout == "strided" else f"blocked C={a.C}",
+        mapping=mapping if mapping == "wide" else f"{mapping} (U={unroll})",
+        flags=flags)
+    info["_kernel"] = "%s (%s)" % (kernel,
+        "fedagg_reduce_step_blocked_f32, EpiStep<FEDAVG>" if fused else
+        "fedagg_reduce_blocked_f32" if a.layout == "blocked" else "fedagg_reduce_f32")
+    info["_traffic"] = load_pmc(a.pmc_json, K, P, kernel,
+                                a.layout if a.layout == "strided" else f"blocked{a.C}",
+                                step_mode)
+    return step, info, 4.0 * K * P * rk.world, (X, avg, cloud, grad)
+
+
+# -- streamed rounds (strong / allreduce) ----------------------------------
+def _pool_rows(a, rk, K, P, C):
+    """Resident rows: --pool-rows, else (allreduce) 200, else (strong) as many
+    of the K rows as fit the free HBM less 16 GiB of headroom."""
+    if a.pool_rows:
+        return min(K, a.pool_rows)
+    if a.mode == "allreduce":
+        return min(K, 200)
+    if rk.rehearsal:
+        return K
+    row_bytes = 4 * ((P + C - 1) // C) * C
+    free, _ = rk.torch.cuda.mem_get_info(rk.dev)
+    fit = max(1, (free - (16 << 30) - 4 * 4 * P) // row_bytes)
+    return int(min(K, fit))
+
+
+def setup_streamed(a, rk, clock):
+    """strong: this rank's column shard of all K clients; allreduce: all P
+    columns of this rank's K clients, then all-reduce of the partial sum.
+    Rows beyond the resident pool are re-reads of it (accumulator chained
+    through acc_in: +8P bytes per extra pass, not counted as algorithmic)."""
+    from fedsim_amd import ops, sharding
+
+    torch = rk.torch
+    if a.mode == "strong":
+        lo, hi = sharding.shard_range(a.P, rk.rank, rk.world, sharding.ALIGN)
+        P, K, K_total = hi - lo, a.K, a.K
+        weights = _weights(K)
+        W = sum(weights)
+    else:
+        P, K, K_total = a.P, a.K, a.K * rk.world
+        all_w = _weights(K_total)
+        weights = all_w[rk.rank * K:(rk.rank + 1) * K]
+        W = sum(all_w)  # the host sums the weights of every rank's clients
+    C = ops.choose_block_cols(P)
+    R = _pool_rows(a, rk, K, P, C)
+    counts = [min(R, K - k0) for k0 in range(0, K, R)]
+    pool = make_pool(rk, R, P, C, seed=3 + rk.rank)
+    w32 = torch.tensor([ops.fl32(v) for v in weights], dtype=torch.float32, device=rk.dev)
+    acc = torch.empty(P, dtype=torch.float32, device=rk.dev)
+    ar_ms = []
+    info = dict(clients_K=K_total, params_per_gpu_P=P, params_total=a.P,
+                pool_rows=R, passes=len(counts),
+                pool_GB=round(4.0 * R * P / 1e9, 1))
+    if rk.rehearsal:
+        info["layout"] = "row-major (rehearsal)"
+
+        def step():
+            for i, n in enumerate(counts):
+                last = i == len(counts) - 1
+                rk.stub(pool[:n], w32[i * R:i * R + n], acc, None if i == 0 else acc,
+                        W if (last and a.mode == "strong") else None)
+            if a.mode == "allreduce":
+                if rk.dist is not None:
+                    rk.dist.all_reduce(acc)
+                acc.div_(ops.fl32(W))
+        info.update(parallelism=("param-shard%d" % rk.world if a.mode == "strong"
+                                 else "client-shard%d+allreduce" % rk.world))
+        total = 4.0 * K * (a.P if a.mode == "strong" else P * rk.world)
+        return step, info, total, (pool,), ar_ms
+
+    sstep, cloud, grad = fedavg_step(rk, P)
+    flags = ops.default_flags(C)
+    fuse_last = a.mode == "strong"  # allreduce: the step needs the global sum
+
+    def one_pass(i, n, last):
+        wv = w32[i * R:i * R + n]
+        acc_in = None if i == 0 else acc
+        if last and fuse_last:
+            nb = 4.0 * n * P + 4.0 * n + 12.0 * P
+            clock.run(nb, lambda: ops.reduce_blocked_step(pool, wv, sstep, B=n, acc_in=acc_in,
+                                                          W=W))
+        else:
+            nb = 4.0 * n * P + 4.0 * n + 4.0 * P
+            clock.run(nb, lambda: ops.reduce_blocked(pool, wv, acc, B=n, acc_in=acc_in,
+                                                     flags=flags))
+
+    def step():
+        for i, n in enumerate(counts):
+            one_pass(i, n, i == len(counts) - 1)
+        if a.mode == "allreduce":
+            if rk.dist is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rk.dist.all_reduce(acc, op=rk.dist.ReduceOp.SUM)
+                e1.record()
+                if clock.on:
+                    ar_ms.append((e0, e1))
+            ops.finalize(acc, W, out=acc)
+            sstep.apply(acc)
+
+    kname = "k_reduce_narrow (fedagg_reduce_blocked_f32 passes%s)" % (
+        " + fedagg_reduce_step_blocked_f32 last pass" if fuse_last else "")
+    info.update(
+        workload=("FedAvg server round, parameter-sharded (config 4): this rank's column "
+                  "shard of every client, exact reduce + divide + SGD step fused into "
+                  "the last pass" if a.mode == "strong" else
+                  "FedAvg server round, client-sharded (config 5): this rank's clients "
+                  "reduced in order into a partial sum, RCCL all-reduce(sum) of 4P bytes, "
+                  "divide by fl32(W), SGD server step"),
+        parallelism=("param-shard%d" % rk.world if a.mode == "strong"
+                     else "client-shard%d+allreduce" % rk.world),
+        mode=("exact (bitwise vs reference CPU)" if a.mode == "strong"
+              else "reordered across ranks (normwise <= 1e-6 vs reference CPU)"),
+        layout=f"blocked C={C}", step="fused" if fuse_last else "split")
+    info["_kernel"] = kname
+    info["_traffic"] = None
+    total = 4.0 * K * (a.P if a.mode == "strong" else P * rk.world)
+    return step, info, total, (pool, acc, cloud, grad), ar_ms
+
+
+def main():
+    argv = sys.argv[1:]
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(a, argv))
+    quiet = _StdoutToStderr()
+    try:
+        _main(a, quiet)
+    finally:
+        quiet.restore()
+
+
+def _main(a, quiet):
+    rk = Rank(a)
+    if a.gpus != rk.world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={rk.world}")
+    clock = KernelClock(rk)
+    ar_ms = []
+    if a.mode == "param":
+        step, info, total_bytes, keep = setup_param(a, rk, clock)
+    else:
+        step, info, total_bytes, keep, ar_ms = setup_streamed(a, rk, clock)
+
+    for _ in range(a.warmup):
+        step()
+    rk.sync()
+    clock.on = True
+    rk.barrier()
+    rk.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    rk.sync()
+    rk.barrier()
+    elapsed = time.perf_counter() - t0
+    clock.on = False
+    nbytes, kern_ms = clock.summary()
+    ar = None
+    if ar_ms:
+        ar = sum(e0.elapsed_time(e1) for e0, e1 in ar_ms) / len(ar_ms)
+    elapsed, kern_ms_max, ar_max = rk.max_over_ranks(
+        elapsed, kern_ms if kern_ms is not None else 0.0, ar if ar is not None else 0.0)
+
+    value = total_bytes * a.steps / elapsed / 1e9
+    kernel = info.pop("_kernel", None)
+    traffic = info.pop("_traffic", None)
     result = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "GB/s",
-        "n_gpus": world,
+        "n_gpus": rk.world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.mode == "strong" else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (x_k = base + eps_k on device, FedAvg int weights U{50..600})",
-        "config": {
-            "workload": ("FedAvg server round, device-resident: exact weighted reduce + divide "
-                         "+ SGD server step in one pass" if fused else
-                         "FedAvg server round, device-resident: exact weighted reduce + divide, "
-                         "then the SGD epilogue kernel"),
-            "step": step_mode,
-            "clients_K": K,
-            "params_per_gpu_P": P,
-            "params_total": P * world,
-            "parallelism": f"param-shard{world}" if world > 1 else "single",
-            "mode": "exact (bitwise vs reference CPU)",
-            "layout": a.layout if a.layout == "strided" else f"blocked C={a.C}",
-            "mapping": mapping if mapping == "wide" else f"{mapping} (U={unroll})",
-            "flags": flags,
-        },
-        "roofline": {
+        "data": ("synthetic (x_k = base + eps_k on device, FedAvg int weights U{50..600})"
+                 if a.mode == "param" else
+                 "synthetic (resident pool of distinct N(0, 0.05) client rows, re-read "
+                 "cyclically; FedAvg int weights U{50..600})"),
+        "config": dict(info, mode_flag=a.mode),
+    }
+    if rk.rehearsal:
+        result["rehearsal"] = "cpu/gloo launcher rehearsal, per-rank reduce = " + a.rehearsal_stub
+        result["roofline"] = None
+    else:
+        result["world_size_seen"] = rk.dist.get_world_size() if rk.dist is not None else 1
+        result["backend"] = rk.dist.get_backend() if rk.dist is not None else None
+        achieved = nbytes / (kern_ms_max * 1e-3) / 1e9
+        result["roofline"] = {
             "bound": "hbm",
-            "kernel": "%s (%s)" % (kernel,
-                "fedagg_reduce_step_blocked_f32, EpiStep<FEDAVG>" if fused else
-                "fedagg_reduce_blocked_f32" if a.layout == "blocked" else "fedagg_reduce_f32"),
+            "kernel": kernel,
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBPS, 4),
             "traffic": traffic,
-            "launch_ms": round(kern_ms, 4),
-            "alg_bytes_per_launch": alg_bytes_launch,
-        },
-    }
-    del X
-    torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(P, a.cpu_baseline_seconds)
-    if rank == 0:
+            "launch_ms": round(kern_ms_max, 4),
+            "alg_bytes_per_launch": nbytes,
+        }
+        if a.mode == "allreduce":
+            result["allreduce"] = dict(
+                ms=round(ar_max, 4) if ar_ms else None,
+                bytes=4 * a.P,
+                share_of_round=round(ar_max / (elapsed / a.steps * 1e3), 4) if ar_ms else None,
+                note="RCCL all-reduce(sum) of the fp32 partial, HIP events on the compute "
+                     "stream around the call (max over ranks); none at N=1 without a "
+                     "process group")
+    del keep, step
+    if not rk.rehearsal:
+        rk.torch.cuda.empty_cache()
+    if rk.rank == 0 and rk.world == 1 and not a.no_cpu_baseline and not rk.rehearsal:
+        result["cpu_baseline"] = cpu_baseline(a.P, a.cpu_baseline_seconds)
+    if rk.rank == 0:
         quiet.restore()
         print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if rk.dist is not None:
+        rk.dist.barrier()
+        rk.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -28,6 +28,16 @@ except Exception:  # pragma: no cover
     _trange = range
 
 
+def _distributed_world() -> int:
+    d = torch.distributed
+    return d.get_world_size() if d.is_available() and d.is_initialized() else 1
+
+
+def _distributed_rank() -> int:
+    d = torch.distributed
+    return d.get_rank() if d.is_available() and d.is_initialized() else 0
+
+
 class CentralFLAlgorithm(object):
     def __init__(
         self,
@@ -89,9 +99,16 @@ class CentralFLAlgorithm(object):
 
         # size each round's HBM ring once for the clients it will receive, and
         # reduce HBM-resident client vectors in place: a message is dropped
-        # right after receive_from_client, so its tensor can be handed over
-        self._aggregator_factory = aggregator_factory or partial(
-            SerialAggregator, expected_rows=sample_count, borrow=True)
+        # right after receive_from_client, so its tensor can be handed over.
+        # Under a torch.distributed group of several ranks (one process per
+        # GPU, every rank running this same round loop) each rank reduces and
+        # steps its own column shard of the model (fedsim_amd.sharding).
+        if aggregator_factory is None:
+            cls = SerialAggregator
+            if _distributed_world() > 1:
+                from ...sharding import ShardedSerialAggregator as cls
+            aggregator_factory = partial(cls, expected_rows=sample_count, borrow=True)
+        self._aggregator_factory = aggregator_factory
         self._progress = progress
         self._server_memory = Storage()
         w = self._server_memory.write
@@ -195,7 +212,8 @@ class CentralFLAlgorithm(object):
             mem, mem.read("global_dataloaders", silent=True), rounds, round_scores,
             metric_logger, mem.read("device"), optimize_reports, deployment_points,
         )
-        if metric_logger is not None:
+        if metric_logger is not None and _distributed_rank() == 0:
+            # ranks of a sharded run report the same scalars: log them once
             apply_on_dict(report_metrics, metric_logger.log_scalar, step=rounds)
         return report_metrics
 

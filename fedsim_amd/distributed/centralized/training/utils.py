@@ -4,8 +4,18 @@
 (fedsim/distributed/centralized/training/utils.py:7-57): divergence -> False,
 weight = ``train_weight`` or ``num_samples[train_split_name]``, skip when the
 weight is <= 0, per-split scalar metrics added with the (sticky) other_weight.
-The reference's defensive ``clone()`` (utils.py:34) is dropped: the aggregator's
-``add`` already snapshots the vector into HBM, so the copy bought nothing.
+The reference's defensive ``clone()`` (utils.py:34) is kept only where it
+changes anything.  ``SerialAggregator.add`` snapshots host vectors (into the
+pinned staging ring) and, by default, HBM vectors (into the ring slab); the
+round driver's aggregator instead *borrows* HBM-resident vectors and reads
+them when the round is reduced.  Borrowing is only sound when the message held
+the sole reference to a tensor that shares its storage with nothing else (a
+fresh ``vectorize_module`` result): a client that reuses one output buffer, or
+keeps the tensor or a view of it, could otherwise change it before the round
+is reduced.  So the vector is cloned here -- the reference's own copy --
+whenever the aggregator would borrow it and that ownership cannot be shown
+(``_handed_over``); borrowing a tensor that is then modified in place anyway is
+caught by its version counter at the drain.
 
 ``fused_server_step`` runs the FedAvg / AdaBest / FedDyn ``optimize`` epilogues
 (fedavg.py:193-208, adabest.py:172-189, feddyn.py:169-194) together with the
@@ -18,6 +28,7 @@ aggregation itself is still the HIP kernel).
 """
 from __future__ import annotations
 
+import sys
 from typing import Optional
 
 import torch
@@ -39,6 +50,8 @@ def serial_aggregation(
     purge_msg=True,
 ):
     params = client_msg["local_params"]
+    if not _handed_over(params) and _would_borrow(aggregator, params):
+        params = params.clone()  # the reference's snapshot (utils.py:34)
     if params.requires_grad:  # detach only when needed: it allocates a tensor object
         params = params.detach()
     diverged = client_msg["diverged"]
@@ -62,6 +75,45 @@ def serial_aggregation(
     if purge_msg:
         del client_msg
     return True
+
+
+def _refcount(t) -> int:
+    return sys.getrefcount(t)
+
+
+def _count_in_callee(t) -> int:
+    return _refcount(t)
+
+
+def _owned_refs() -> int:
+    """References to a tensor held only by a message dict and one local
+    variable, seen from a function it is passed to, as serial_aggregation
+    passes ``params`` to _handed_over (measured, not assumed: CPython's count
+    includes the calls' own argument references)."""
+    msg = {"local_params": torch.empty(1)}
+    params = msg["local_params"]
+    return _count_in_callee(params)
+
+
+_OWNED_REFS = _owned_refs()
+
+
+def _handed_over(t: torch.Tensor) -> bool:
+    """Whether the client message holds the only reference to ``t`` and no
+    other tensor (view, base, alias) shares its storage.  Called with
+    serial_aggregation's ``params`` local, as _owned_refs measures."""
+    if not isinstance(t, torch.Tensor) or t._base is not None:
+        return False
+    if _refcount(t) > _OWNED_REFS:
+        return False
+    # one TensorImpl + the temporary storage object created here
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= 2
+
+
+def _would_borrow(aggregator, t) -> bool:
+    opts = getattr(aggregator, "_opts", None)
+    return (isinstance(aggregator, _DeviceSerialAggregator) and opts is not None
+            and opts.borrow and isinstance(t, torch.Tensor) and t.device.type == "cuda")
 
 
 def pop_average(aggregator, key="local_params") -> torch.Tensor:

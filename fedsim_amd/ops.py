@@ -377,11 +377,20 @@ class ServerStep(object):
                     (momentum_buf, "momentum_buf"), (grad_out, "grad_out"), (avg_out, "avg_out"))
         for t, n in operands:
             if t is not None:
-                _require_hip_f32(t, n)
+                # the HIP-device check is made where a kernel is launched on
+                # the operands (apply / reduce_*_step): a ServerStep is also
+                # the description a sharded aggregator narrows per rank
+                if not isinstance(t, torch.Tensor) or t.dtype != torch.float32:
+                    raise TypeError(f"{n} must be a float32 tensor")
                 if t.numel() != P or not t.is_contiguous():
                     raise ValueError(f"{n} must be contiguous with {P} elements")
                 if t.device != cloud.device:
                     raise ValueError(f"{n} is on {t.device}, cloud on {cloud.device}")
+        self.algo = algo
+        self.operands = {n: t for t, n in operands if t is not None}
+        self._scalars = dict(lr=lr, momentum=momentum, dampening=dampening,
+                             weight_decay=weight_decay, nesterov=nesterov, maximize=maximize,
+                             coef=coef, momentum_init=momentum_init)
         self._keep = [t for t, _ in operands if t is not None]  # alive until launched
         self.sgd = _native.SgdParams(fl32(-lr), fl32(momentum), fl32(1 - dampening),
                                      fl32(weight_decay), int(bool(nesterov)),
@@ -395,10 +404,25 @@ class ServerStep(object):
         """Every operand 16-B aligned (required by the fused entry)."""
         return all(t.data_ptr() % 16 == 0 for t in self._keep)
 
+    def narrow(self, lo: int, hi: int) -> "ServerStep":
+        """The same step restricted to parameters [lo, hi) (views of every
+        operand): what one rank of a parameter-sharded round runs."""
+        views = {n: t[lo:hi] for n, t in self.operands.items()}
+        cloud = views.pop("cloud")
+        return ServerStep(self.algo, cloud, **self._scalars, **views)
+
+    def outputs(self):
+        """The operands the step writes (cloud and whichever of aux /
+        avg_prev / momentum_buf / grad_out / avg_out it was given)."""
+        return [t for n, t in self.operands.items()]
+
     def apply(self, avg: torch.Tensor) -> torch.Tensor:
         _require_hip_f32(avg, "avg")
+        _require_hip_f32(self.cloud, "cloud")
         if avg.numel() != self.P or not avg.is_contiguous():
             raise ValueError(f"avg must be contiguous with {self.P} elements")
+        if avg.device != self.cloud.device:
+            raise ValueError(f"avg is on {avg.device}, cloud on {self.cloud.device}")
         a = self.args
         rc = _native.load().fedagg_server_step_f32(
             a.algo, avg.data_ptr(), a.coef, a.cloud, a.aux, a.avg_prev, a.momentum_buf,
@@ -406,6 +430,11 @@ class ServerStep(object):
             _stream_ptr(self.cloud.device),
         )
         check(rc, "fedagg_server_step_f32")
+        avg_out = self.operands.get("avg_out")
+        if avg_out is not None and avg_out.data_ptr() != avg.data_ptr():
+            # the stored-average kernel has no avg_out operand: the fused
+            # entries write it in their epilogue, this path copies it
+            avg_out.copy_(avg)
         return self.cloud
 
 
@@ -466,6 +495,9 @@ def reduce_blocked_step(
     _require_hip_f32(w32, "w32")
     if Xb.dim() != 3 or not Xb.is_contiguous():
         raise ValueError("Xb must be a contiguous [nblk, Kcap, C] tensor")
+    if step.cloud.device != Xb.device:
+        raise ValueError(f"the step's operands are on {step.cloud.device}, the slab on "
+                         f"{Xb.device}")
     nb, Kcap, C = Xb.shape
     P = step.P
     if nb != (P + C - 1) // C:
@@ -523,6 +555,7 @@ def reduce_rows_step(
     validated every row (the aggregator does at ``add``), skip the per-row
     checks."""
     _require_hip_f32(w32, "w32")
+    _require_hip_f32(step.cloud, "cloud")
     P, dev = step.P, step.cloud.device
     B = len(rows)
     for i, r in enumerate(() if checked else rows):

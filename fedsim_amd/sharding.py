@@ -19,8 +19,16 @@ ROCm, over xGMI).  Three modes:
               the divide by fl32(W).  Summation order changes, so parity is
               normwise (||y - y_ref|| / ||y_ref|| <= 1e-6).  (Config 5.)
 
-The per-rank reduction is the HIP kernel (``ops.reduce_slab``); ``local_reduce``
-can be injected so the host-side protocol is testable with gloo on CPU.
+The per-rank reduction is the HIP kernel: ``ops.reduce_blocked`` on a
+column-blocked slab ([nblk, Kcap, C], the layout the aggregator packs into and
+the bench times), ``ops.reduce_slab`` on a row-major [K, P] view;
+``param_sharded_step`` runs the round's server step fused into the shard's
+pass (fedagg_reduce_step_blocked_f32).  ``local_reduce`` can be injected so the
+host-side protocol is testable with gloo on CPU.
+
+On the plugin surface, ``ShardedSerialAggregator`` is the SerialAggregator
+drop-in whose tensor keys are parameter-sharded over the ranks of a process
+group (see its docstring).
 """
 from __future__ import annotations
 
@@ -46,7 +54,28 @@ def shard_range(n: int, rank: int, world: int, align: int = 1):
     return lo, hi
 
 
+def shard_span(n: int, rank: int, world: int, align: int = ALIGN):
+    """[lo, hi) of ``n`` columns for ``rank`` when every shard but the last has
+    the same width S = ceil(ceil(n / align) / world) * align: equal widths let
+    the ranks exchange their shards with one all-gather of world * S columns.
+    A rank past the end gets an empty span (lo == hi == n)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    S = shard_width(n, world, align)
+    return min(n, rank * S), min(n, (rank + 1) * S)
+
+
+def shard_width(n: int, world: int, align: int = ALIGN) -> int:
+    units = (n + align - 1) // align
+    return (units + world - 1) // world * align
+
+
 def _hip_reduce(X, w32, out, acc_in=None, W=None, flags=0):
+    """The per-rank HIP reduction: column-blocked slab ([nblk, Kcap, C], the
+    tuned layout) or a row-major [K, P] view."""
+    if X.dim() == 3:
+        return ops.reduce_blocked(X, w32, out, B=min(X.shape[1], w32.numel()), acc_in=acc_in,
+                                  W=W, flags=flags or ops.default_flags(X.shape[2]))
     return ops.reduce_slab(X, w32, out, acc_in=acc_in, W=W, P=out.numel(), flags=flags)
 
 
@@ -54,6 +83,26 @@ def param_sharded(X_shard: torch.Tensor, w32: torch.Tensor, W, out_shard: torch.
                   local_reduce: Callable = _hip_reduce, flags: int = 0) -> torch.Tensor:
     """Reduce this rank's column shard of all K clients (no collective)."""
     return local_reduce(X_shard, w32, out_shard, None, W, flags)
+
+
+def param_sharded_step(Xb_shard: torch.Tensor, w32: torch.Tensor, W, step: "ops.ServerStep",
+                       B: Optional[int] = None, acc_in: Optional[torch.Tensor] = None,
+                       avg: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One rank's share of a parameter-sharded round: reduce this rank's
+    column shard (column-blocked slab [nblk, Kcap, C]) of B clients, divide by
+    fl32(W) and run the server step on the shard's slice of the cloud
+    (``step`` = the full step narrowed to the shard, ServerStep.narrow).  One
+    pass (fedagg_reduce_step_blocked_f32) where ops.fuse_step_pays, else the
+    stored average (``avg``, allocated if None) and fedagg_server_step_f32;
+    same bits either way.  No collective; bitwise equal to the reference."""
+    B = Xb_shard.shape[1] if B is None else B
+    if ops.fuse_step_pays(step.P, B) and ops.can_fuse_step(Xb_shard, step):
+        return ops.reduce_blocked_step(Xb_shard, w32, step, B=B, acc_in=acc_in, W=W)
+    if avg is None:
+        avg = torch.empty(step.P, dtype=torch.float32, device=Xb_shard.device)
+    ops.reduce_blocked(Xb_shard, w32, avg, B=B, acc_in=acc_in, W=W,
+                       flags=ops.default_flags(Xb_shard.shape[2]))
+    return step.apply(avg)
 
 
 def client_sharded_allreduce(X_local: torch.Tensor, w32_local: torch.Tensor, W,
@@ -106,3 +155,166 @@ def client_sharded_chain(X_local: torch.Tensor, w32_local: torch.Tensor, W,
 
 def weights_fp32(weights: Sequence, device) -> torch.Tensor:
     return torch.tensor([ops.fl32(w) for w in weights], dtype=torch.float32, device=device)
+
+
+# ---------------------------------------------------------------------------
+# plugin surface: a parameter-sharded SerialAggregator
+# ---------------------------------------------------------------------------
+from .utils.aggregators import SerialAggregator, _DeviceEntry, _hip_device, _TensorEntry  # noqa: E402
+
+
+def _group_rank_world(group):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    if group is not None:
+        raise RuntimeError("a process group was given but torch.distributed is not initialised")
+    return 0, 1
+
+
+class _ShardEntry(_TensorEntry):
+    """One tensor-valued key of a ShardedSerialAggregator: this rank reduces
+    columns [lo, hi) of every client vector (``inner``, a one-GPU entry on its
+    own device); results are assembled with one all-gather of the equal-width
+    shards."""
+
+    def __init__(self, agg: "ShardedSerialAggregator", value: torch.Tensor):
+        self.agg = agg
+        self.shape = tuple(value.shape)
+        self.P = value.numel()
+        self.out_device = value.device
+        self.lo, self.hi = shard_span(self.P, agg._rank, agg._world)
+        self.S = shard_width(self.P, agg._world)
+        self.cur_w = 0
+        self.inner = agg._shard_entry(value.reshape(-1)[self.lo:self.hi]) \
+            if self.hi > self.lo else None
+        self.dev = self.inner.dev if self.inner is not None else agg._device_for(value)
+
+    def add(self, value: torch.Tensor, weight) -> None:
+        new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
+        if tuple(value.shape) != self.shape:
+            raise ValueError(
+                f"tensor of shape {tuple(value.shape)} added to a key aggregating {self.shape}")
+        if self.inner is not None:
+            src = value.detach() if value.requires_grad else value
+            self.inner.add(src.reshape(-1)[self.lo:self.hi], weight)
+        self.cur_w = new_w
+
+    # -- exchange -----------------------------------------------------------
+    def _gather_into(self, full: torch.Tensor, part: Optional[torch.Tensor]) -> torch.Tensor:
+        """full[lo:hi] = part on this rank, then every rank's shard into
+        ``full`` (one all-gather of world x S columns)."""
+        if part is not None and part.data_ptr() != full[self.lo:self.hi].data_ptr():
+            full[self.lo:self.hi].copy_(part.reshape(-1))
+        if self.agg._world == 1:
+            return full
+        # gloo has no all-gather of HIP tensors: such groups exchange the
+        # shards through host memory (RCCL groups gather in HBM over xGMI)
+        via_host = full.device.type == "cuda" and \
+            dist.get_backend(self.agg._group) == dist.Backend.GLOO
+        mine = torch.zeros(self.S, dtype=full.dtype, device="cpu" if via_host else full.device)
+        mine[: self.hi - self.lo].copy_(full[self.lo:self.hi])
+        ws = mine.new_empty(self.agg._world * self.S)
+        dist.all_gather_into_tensor(ws, mine, group=self.agg._group)
+        full.copy_(ws[: self.P])
+        return full
+
+    def _assemble(self, part: Optional[torch.Tensor]) -> torch.Tensor:
+        full = torch.empty(self.P, dtype=torch.float32, device=self.dev)
+        self._gather_into(full, part)
+        return full
+
+    def _deliver(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.view(self.shape)
+        return t if t.device == self.out_device else t.to(self.out_device)
+
+    # -- reference semantics --------------------------------------------------
+    def get(self) -> torch.Tensor:
+        return self._deliver(self._assemble(None if self.inner is None else self.inner.get()))
+
+    def get_sum(self) -> torch.Tensor:
+        part = None if self.inner is None else self.inner.get_sum()
+        return self._deliver(self._assemble(part))
+
+    def pop(self, on_device: bool = False) -> torch.Tensor:
+        part = None if self.inner is None else self.inner.pop(on_device=True)
+        full = self._assemble(part)
+        return full.view(self.shape) if on_device else self._deliver(full)
+
+    def pop_step(self, step: ops.ServerStep) -> None:
+        """This rank's shard of pop + server step (ServerStep.narrow), then
+        every operand the step wrote is re-assembled on every rank."""
+        if self.inner is not None:
+            self.inner.pop_step(step.narrow(self.lo, self.hi))
+        for t in step.outputs():
+            self._gather_into(t, None)
+
+
+class ShardedSerialAggregator(SerialAggregator):
+    """Parameter-sharded drop-in for the reference SerialAggregator
+    (fedsim/utils/aggregators.py:11-144) over the ranks of a process group,
+    one process per GPU (the reference round loop it serves is
+    fedsim/distributed/centralized/centralized_fl_algorithm.py:411-443).
+
+    Every rank runs the same round (SPMD) and is handed every client vector;
+    rank g keeps only columns [lo_g, hi_g) of each (``shard_span``: 64-column
+    aligned, equal widths but the last):
+
+    * a host vector crosses PCIe as that slice only, on this GPU's own copy
+      stream and link, so N ranks ingest over N links at once;
+    * a vector already in this GPU's HBM is reduced in place (``borrow``) or
+      packed from there; the slice of a 256-B aligned vector stays aligned;
+    * the reduction is the one-GPU path on the slice (column-blocked ring
+      slab or borrowed rows, exact mode), so every column keeps the reference's
+      summation order: results are BIT-EXACT, with no collective on the data
+      path;
+    * ``pop_step`` runs the round's server step on the slice (fused into the
+      last pass where that pays) and then assembles every operand it wrote
+      (cloud, its pseudo-gradient, aux / momentum state) with one all-gather
+      each, so every rank holds the full new model for the next round;
+    * ``get`` / ``get_sum`` / ``pop`` assemble the average the same way and
+      deliver it on the device the values came from.
+
+    Scalar keys (the per-split metrics) stay on the host with the
+    reference's arithmetic, identically on every rank.
+
+    Args:
+        group: the torch.distributed group (default: the default group; a
+            single process with no group is world 1).
+        entry_factory: TEST HOOK.  ``entry_factory(slice, agg)`` builds the
+            per-rank state of a key instead of the HIP entry, so the protocol
+            can be rehearsed with gloo on CPU (tests/test_sharding_gloo.py).
+        **kwargs: SerialAggregator's options, applied to each rank's slice.
+    """
+
+    def __init__(self, group=None, entry_factory: Optional[Callable] = None, **kwargs) -> None:
+        super().__init__(**kwargs)
+        self._group = group
+        self._rank, self._world = _group_rank_world(group)
+        self._entry_factory = entry_factory
+
+    def _device_for(self, value: torch.Tensor) -> torch.device:
+        if self._entry_factory is not None:
+            return value.device
+        return _hip_device(value, self._opts.device)
+
+    def _shard_entry(self, part: torch.Tensor) -> _TensorEntry:
+        if self._entry_factory is not None:
+            return self._entry_factory(part, self)
+        dev = _hip_device(part, self._opts.device)
+        return _DeviceEntry(part, dev, self._opts, self, out_device=dev)
+
+    def _new_entry(self, value: torch.Tensor) -> _TensorEntry:
+        return _ShardEntry(self, value)
+
+    @property
+    def rank(self) -> int:
+        return self._rank
+
+    @property
+    def world_size(self) -> int:
+        return self._world
+
+    def shard_of(self, key):
+        """[lo, hi) columns this rank reduces for a tensor key."""
+        e = self._entry(key)
+        return (e.lo, e.hi) if isinstance(e, _ShardEntry) else None

@@ -159,14 +159,29 @@ class _Options(object):
         self.fast = fast
 
 
-class _DeviceEntry(object):
-    """One tensor-valued key: fp32 running sum in HBM + a ring of pending
-    client rows in a column-blocked slab [ceil(P/C), R, C] (include/fedagg.h)."""
+class _TensorEntry(object):
+    """What SerialAggregator needs from the state of one tensor-valued key:
+    ``add(value, weight)``, ``get()``, ``get_sum()``, ``pop(on_device)``,
+    ``pop_step(step)``, the running Python weight ``cur_w`` and the device
+    ``dev`` the reduction runs on.  _DeviceEntry is the one-GPU key;
+    fedsim_amd.sharding._ShardEntry spreads a key's columns over the ranks of
+    a process group."""
 
-    def __init__(self, value: torch.Tensor, dev: torch.device, opts: _Options, agg):
+    cur_w = 0
+    dev = None
+
+
+class _DeviceEntry(_TensorEntry):
+    """One tensor-valued key: fp32 running sum in HBM + a ring of pending
+    client rows in a column-blocked slab [ceil(P/C), R, C] (include/fedagg.h).
+    ``out_device``: where get / pop deliver (default: the first value's
+    device, as the reference's tensors stay where they were added)."""
+
+    def __init__(self, value: torch.Tensor, dev: torch.device, opts: _Options, agg,
+                 out_device: Optional[torch.device] = None):
         self.shape = tuple(value.shape)
         self.P = value.numel()
-        self.out_device = value.device
+        self.out_device = value.device if out_device is None else out_device
         self.dev = dev
         self.C = opts.block_cols or ops.choose_block_cols(self.P)
         self.nblk = (self.P + self.C - 1) // self.C
@@ -422,20 +437,23 @@ class SerialAggregator(object):
     def _ingest(dev) -> _Ingest:
         return _ingest_for(dev)
 
+    def _new_entry(self, value: torch.Tensor) -> _TensorEntry:
+        """State of a new tensor-valued key (sharded aggregators override)."""
+        return _DeviceEntry(value, _hip_device(value, self._opts.device), self._opts, self)
+
     @staticmethod
     def _is_device_value(value) -> bool:
         return isinstance(value, torch.Tensor) and value.dim() > 0
 
     def add(self, key, value, weight=None):
         entry = self._members.get(key)
-        if isinstance(entry, _DeviceEntry):
+        if isinstance(entry, _TensorEntry):
             if not self._is_device_value(value):
                 raise TypeError(f"key {key!r} aggregates tensors; got {type(value).__name__}")
             entry.add(value, weight)
             return
         if entry is None and self._is_device_value(value):
-            dev = _hip_device(value, self._opts.device)
-            entry = _DeviceEntry(value, dev, self._opts, self)
+            entry = self._new_entry(value)
             entry.add(value, weight)
             self._members[key] = entry
             return
@@ -456,7 +474,7 @@ class SerialAggregator(object):
 
     def get(self, key):
         e = self._entry(key)
-        if isinstance(e, _DeviceEntry):
+        if isinstance(e, _TensorEntry):
             return e.get()
         v, w = e
         if w is None or w == 0:
@@ -465,13 +483,13 @@ class SerialAggregator(object):
 
     def get_sum(self, key):
         e = self._entry(key)
-        if isinstance(e, _DeviceEntry):
+        if isinstance(e, _TensorEntry):
             return e.get_sum()
         return e[0]
 
     def get_weight(self, key):
         e = self._entry(key)
-        if isinstance(e, _DeviceEntry):
+        if isinstance(e, _TensorEntry):
             return e.cur_w
         return e[1]
 
@@ -481,7 +499,7 @@ class SerialAggregator(object):
     def pop(self, key):
         e = self._entry(key)
         del self._members[key]
-        if isinstance(e, _DeviceEntry):
+        if isinstance(e, _TensorEntry):
             return e.pop()
         v, w = e
         if w is None or w == 0:
@@ -492,7 +510,7 @@ class SerialAggregator(object):
         """``pop`` that leaves a tensor result in HBM (no D2H), for the fused
         server step (not part of the reference API)."""
         e = self._entry(key)
-        if not isinstance(e, _DeviceEntry):
+        if not isinstance(e, _TensorEntry):
             return self.pop(key)
         del self._members[key]
         return e.pop(on_device=True)
@@ -500,7 +518,7 @@ class SerialAggregator(object):
     def device_of(self, key) -> Optional[torch.device]:
         """HIP device holding a tensor key's sum (None for host keys)."""
         e = self._entry(key)
-        return e.dev if isinstance(e, _DeviceEntry) else None
+        return e.dev if isinstance(e, _TensorEntry) else None
 
     def pop_step(self, key, step: ops.ServerStep) -> None:
         """``pop(key)`` and ``step.apply(average)`` in one pass over the
@@ -508,7 +526,7 @@ class SerialAggregator(object):
         of FedAvg / AdaBest / FedNova / FedDyn optimize runs in the epilogue of
         the round's last reduction, so the average is never stored."""
         e = self._entry(key)
-        if not isinstance(e, _DeviceEntry):
+        if not isinstance(e, _TensorEntry):
             avg = self.pop(key)
             step.apply(avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
             return

@@ -296,7 +296,10 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
  * followed by fedagg_server_step_f32 in one pass.  This is the zero-copy
  * round of HBM-resident client vectors (GPU-local training): no pack, no
  * slab; SerialAggregator.add (aggregators.py:23-40) only records the row.
- * Flags as for fedagg_reduce_step_blocked_f32 (FEDAGG_NT honoured).
+ * Flags as for fedagg_reduce_step_blocked_f32.  FEDAGG_NT is read only by
+ * the wide mapping (FEDAGG_MAP_WIDE); the narrow mappings (the default at
+ * every P) and the flat path of rows >= 2^30 columns always load the client
+ * rows non-temporally (measured +4.7 % at 1000 x 25 M).
  */
 int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_t B,
                                 int64_t P, const float* acc_in, float W32, int flags,

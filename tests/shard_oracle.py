@@ -1,0 +1,60 @@
+"""Per-rank state of a ShardedSerialAggregator key with the C oracle as the
+reducer and server step (TEST INFRASTRUCTURE): lets the parameter-sharded
+plugin protocol -- slicing, the Python weight sums, the narrowed server step
+and the all-gathers -- run on CPU over gloo.  The arithmetic is the oracle's
+(oracle/fedagg_ref.c), which reproduces the reference's bits; the HIP entry
+replaces this class on the GPU (tests/test_gpu_sharding.py)."""
+import numpy as np
+import torch
+
+from fedsim_amd.utils.aggregators import _TensorEntry
+from oracle import ref
+
+
+CALLS = {"add": 0, "pop_step": 0}
+
+
+class OracleEntry(_TensorEntry):
+    def __init__(self, part, agg):
+        self.P = part.numel()
+        self.dev = torch.device("cpu")
+        self.rows = []
+        self.ws = []
+        self.cur_w = 0
+
+    def add(self, value, weight):
+        new_w = self.cur_w + weight
+        CALLS["add"] += 1
+        # snapshot, as the HIP entry does at add time
+        self.rows.append(np.array(value.detach().cpu().numpy(), dtype=np.float32, copy=True))
+        self.ws.append(weight)
+        self.cur_w = new_w
+
+    def _weighted(self):
+        return not (self.cur_w is None or self.cur_w == 0)
+
+    def _reduce(self, W=None):
+        return torch.from_numpy(ref.reduce(np.stack(self.rows), self.ws, W=W))
+
+    def get(self):
+        return self._reduce(self.cur_w if self._weighted() else None)
+
+    def get_sum(self):
+        return self._reduce()
+
+    def pop(self, on_device=False):
+        return self.get()
+
+    def pop_step(self, step):
+        """The ABI's own step description (fedagg_step_args) handed to the
+        oracle's server step: the CPU operands' pointers are host pointers."""
+        CALLS["pop_step"] += 1
+        avg = self.pop().contiguous()
+        a, s = step.args, step.sgd
+        ref.lib().ref_server_step_f32(a.algo, avg.data_ptr(), a.coef, a.cloud, a.aux, a.avg_prev,
+                                      a.momentum_buf, a.momentum_init, a.grad_out, s.neg_lr,
+                                      s.momentum, s.one_minus_dampening, s.weight_decay,
+                                      s.nesterov, s.maximize, step.P)
+        avg_out = step.operands.get("avg_out")
+        if avg_out is not None:
+            avg_out.copy_(avg)

@@ -1,0 +1,58 @@
+"""bench.py's own N-rank launcher (``--gpus N`` without torch.distributed.run),
+rehearsed on CPU over gloo with a stub per-rank reduction
+(tests/bench_stub.py): exactly ONE JSON line on stdout, from rank 0, carrying
+n_gpus = N; every mode; a failing rank fails the whole run instead of hanging
+it.  The GPU run of the same launcher is in tests/test_gpu_bench.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=240):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args],
+                          cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("mode", ["param", "strong", "allreduce"])
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_launcher_one_line(mode, gpus):
+    r = _bench("--gpus", str(gpus), "--mode", mode, "--rehearsal-stub",
+               "tests.bench_stub:reduce", "--K", "9", "--P", "1000", "--steps", "2",
+               "--warmup", "1", "--pool-rows", "4")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == gpus
+    assert d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == ("strong" if mode == "strong" else "weak")
+    assert d["config"]["mode_flag"] == mode
+    if mode == "strong":
+        assert d["config"]["params_total"] == 1000
+    if mode == "allreduce":
+        assert d["config"]["clients_K"] == 9 * gpus
+    assert d["value"] > 0
+
+
+def test_launcher_rank_failure_fails_run():
+    r = _bench("--gpus", "2", "--rehearsal-stub", "tests.bench_stub:fail_on_rank1", "--K", "4",
+               "--P", "256", "--steps", "1", "--warmup", "1", timeout=120)
+    assert r.returncode != 0
+    assert "injected failure on rank 1" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_world_mismatch_rejected():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--rehearsal-stub", "tests.bench_stub:reduce", "--K", "2", "--P", "64"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -107,13 +107,15 @@ def test_borrowed_rows_on_another_stream(dev):
 
 @pytest.mark.parametrize("algo", ["fedavg", "adabest", "feddyn"])
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
-def test_borrowed_pop_step_matches_two_step(algo, momentum, dev):
+@pytest.mark.parametrize("P", [70_001, 70_002])
+def test_borrowed_pop_step_matches_two_step(algo, momentum, P, dev):
     """pop_step over borrowed rows (one fedagg_reduce_step_rows_f32 launch)
-    == pop + fedagg_server_step_f32, bitwise, for every algorithm epilogue."""
+    == pop + fedagg_server_step_f32, bitwise, for every algorithm epilogue.
+    Odd P runs one column per lane; even P two (the early-operand code)."""
     from fedsim_amd import ops
     from fedsim_amd.utils import SerialAggregator
 
-    K, P = 9, 70_001
+    K = 9
     X = V.client_rows("realistic", K, P, 4)
     w = V.client_weights("fedavg", K, 4)
     cloud0 = torch.from_numpy(V.cloud_vector(P, 5)).to(dev)
@@ -237,8 +239,10 @@ def test_pop_step_split_policy_bitwise(borrow, algo, dev):
     outs = []
     for via in ("aggregator", "fused_entry"):
         cloud, aux, grad = cloud0.clone(), aux0.clone(), torch.empty_like(cloud0)
+        avg_out = torch.full_like(cloud0, float("nan"))
         step = ops.ServerStep(algo, cloud, lr=0.3, coef=0.6,
-                              aux=None if algo == "fedavg" else aux, grad_out=grad)
+                              aux=None if algo == "fedavg" else aux, grad_out=grad,
+                              avg_out=avg_out)
         if via == "aggregator":
             agg = SerialAggregator(borrow=borrow)
             for k in range(K):
@@ -247,11 +251,13 @@ def test_pop_step_split_policy_bitwise(borrow, algo, dev):
         else:
             w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
             ops.reduce_rows_step(rows, w32, step, W=sum(w))
-        outs.append([t.cpu().numpy() for t in (cloud, aux, grad)])
+        outs.append([t.cpu().numpy() for t in (cloud, aux, grad, avg_out)])
     for a, b in zip(*outs):
         np.testing.assert_array_equal(bits(a), bits(b))
+    avg = ref.reduce(X, w, W=sum(w))
+    # avg_out is written on the split path too (ServerStep.apply copies it)
+    np.testing.assert_array_equal(bits(outs[0][3]), bits(avg))
     if algo == "fedavg":
-        avg = ref.reduce(X, w, W=sum(w))
         np.testing.assert_array_equal(bits(outs[0][0]),
                                       bits(ref.fedavg_sgd(avg, cloud0.cpu().numpy(), 0.3)))
 
@@ -280,3 +286,120 @@ def test_borrowed_rows_two_pieces_bitwise(K, P, dev):
                          W=sum(w))
     np.testing.assert_array_equal(bits(cloud.cpu().numpy()),
                                   bits(ref.fedavg_sgd(avg, cloud0, 0.3)))
+
+
+@pytest.mark.parametrize("init", [True, False])
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("algo", ["adabest", "feddyn"])
+def test_borrowed_rows_two_pieces_step_algos(algo, momentum, init, dev):
+    """The two-piece kernel with the step operands read early and pinned
+    (three per piece for AdaBest / FedDyn with momentum): fused step vs the
+    oracle's server step, bitwise, with a fresh and a carried momentum
+    buffer, at a P with a ragged two-piece tail."""
+    from fedsim_amd import ops
+
+    K, P = 21, (1 << 22) + 130
+    X = V.client_rows("realistic", K, P, 33)
+    w = V.client_weights("fedavg", K, 33)
+    rows = [torch.from_numpy(X[k].copy()).to(dev) for k in range(K)]
+    w32 = torch.tensor([ops.fl32(v) for v in w], device=dev)
+    cloud0, aux0 = V.cloud_vector(P, 34), V.cloud_vector(P, 35)
+    opt = dict(lr=0.3, momentum=momentum)
+    st = ref.ServerState(algo, cloud0, opt, aux=aux0, coef=0.6)
+    buf0 = None
+    if momentum and not init:  # carry a buffer from a first oracle step
+        st.step(V.cloud_vector(P, 36))
+        buf0 = st.buf.copy()
+    cloud_in = st.cloud.copy()
+    aux_in = st.aux.copy()
+    avg = ref.reduce(X, w, W=sum(w))
+    st.step(avg)
+    cloud = torch.from_numpy(cloud_in).to(dev)
+    aux = torch.from_numpy(aux_in).to(dev)
+    grad = torch.empty_like(cloud)
+    buf = None
+    if momentum:
+        buf = torch.from_numpy(buf0).to(dev) if buf0 is not None else torch.empty_like(cloud)
+    avg_prev = torch.empty_like(cloud) if algo == "feddyn" else None
+    step = ops.ServerStep(algo, cloud, lr=0.3, momentum=momentum, coef=0.6, aux=aux,
+                          avg_prev=avg_prev, momentum_buf=buf, momentum_init=buf0 is None,
+                          grad_out=grad)
+    ops.reduce_rows_step(rows, w32, step, W=sum(w))
+    np.testing.assert_array_equal(bits(cloud.cpu().numpy()), bits(st.cloud))
+    np.testing.assert_array_equal(bits(aux.cpu().numpy()), bits(st.aux))
+    np.testing.assert_array_equal(bits(grad.cpu().numpy()), bits(st.grad))
+    if momentum:
+        np.testing.assert_array_equal(bits(buf.cpu().numpy()), bits(st.buf))
+    if algo == "feddyn":
+        np.testing.assert_array_equal(bits(avg_prev.cpu().numpy()), bits(st.avg_prev))
+
+
+_REUSED = {}
+
+
+def _reuse_buffer_send(*args, **kwargs):
+    """A client that writes every update into ONE persistent device buffer
+    and returns that buffer (legal under the reference, which clones each
+    message at training/utils.py:34)."""
+    from oracle import synthetic_fl as S
+
+    msg = S.synthetic_send_to_server(*args, **kwargs)
+    v = msg["local_params"]
+    buf = _REUSED.get(v.device)
+    if buf is None:
+        buf = _REUSED[v.device] = torch.empty_like(v)
+    buf.copy_(v)
+    msg["local_params"] = buf
+    return msg
+
+
+def test_client_reusing_its_buffer_matches_reference(dev):
+    """The round driver's aggregator borrows HBM vectors; serial_aggregation
+    must clone a vector whose ownership it cannot show, so a buffer-reusing
+    client gets the reference's 5-round FedAvg trajectory bit for bit (no
+    error, no stale rows), while a fresh vector is still borrowed."""
+    import json
+    import os
+    import random
+    from functools import partial
+
+    from conftest import GOLDEN_DIR
+    from fedsim_amd.distributed.centralized.training import FedAvg
+    from oracle import synthetic_fl as S
+
+    with open(os.path.join(GOLDEN_DIR, "rounds.json")) as f:
+        run = [r for r in json.load(f)["runs"] if r["id"] == "r0"][0]
+    with np.load(os.path.join(GOLDEN_DIR, "rounds.npz"), allow_pickle=False) as z:
+        want = z["r0/cloud"]
+
+    class Reusing(S.make_algorithm(FedAvg)):
+        send_to_server = _reuse_buffer_send
+
+    random.seed(S.RANDOM_SEED)
+    torch.manual_seed(S.TORCH_SEED)
+    alg = Reusing(data_manager=S.FakeDataManager(), metric_logger=None,
+                  num_clients=S.NUM_CLIENTS, sample_scheme="uniform", sample_rate=S.SAMPLE_RATE,
+                  model_def=S.TinyModel, epochs=1, criterion_def="CrossEntropyScore",
+                  optimizer_def=partial(torch.optim.SGD, **run["opt_kwargs"]), device="cuda")
+    scores = alg.train(rounds=S.ROUNDS)
+    got = alg.get_server_storage().read("cloud_params").detach().cpu().numpy()
+    np.testing.assert_array_equal(bits(got), bits(want))
+    assert {k: float(v) for k, v in scores.items()} == run["scores"]
+
+    # a fresh, sole-owned vector is borrowed (no copy), a kept one is cloned
+    from fedsim_amd.distributed.centralized.training import serial_aggregation
+    from fedsim_amd.utils import SerialAggregator
+
+    agg = SerialAggregator(borrow=True)
+    msg = dict(local_params=torch.ones(4096, device=dev), num_samples=dict(train=3),
+               diverged=False, metrics=dict())
+    ptr = msg["local_params"].data_ptr()
+    assert serial_aggregation(None, 0, msg, "train", agg)
+    entry = agg._members["local_params"]
+    assert entry.borrowed[0][0].data_ptr() == ptr
+    kept = torch.ones(4096, device=dev)
+    msg = dict(local_params=kept, num_samples=dict(train=3), diverged=False, metrics=dict())
+    assert serial_aggregation(None, 1, msg, "train", agg)
+    assert entry.borrowed[1][0].data_ptr() != kept.data_ptr()
+    kept.fill_(5.0)  # the caller still owns it and may change it
+    assert torch.equal(agg.pop("local_params"), torch.ones(4096, device=dev))

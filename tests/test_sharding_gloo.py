@@ -5,6 +5,10 @@ decomposition, the collectives and the ordering guarantees:
   param     concatenated shards == single-device reference, bitwise
   chain     client-sharded pipeline == single-device reference, bitwise
   allreduce client-sharded partial sums: normwise <= 1e-6 + forward-error bound
+and, on the plugin surface, ShardedSerialAggregator (the per-rank state is the
+C oracle, tests/shard_oracle.py): the reference's own 5-round trajectories of
+FedAvg / AdaBest / FedNova / FedDyn through CentralFLAlgorithm, every rank
+holding the full model after each round, bitwise against the goldens.
 """
 import os
 import socket
@@ -118,3 +122,93 @@ def test_shard_range_covers_and_aligns():
             for (a, b), (c, d) in zip(spans, spans[1:]):
                 assert b == c and a <= b
                 assert b % 64 == 0 or b == n
+
+
+# ---------------------------------------------------------------------------
+# ShardedSerialAggregator through the round driver
+# ---------------------------------------------------------------------------
+def _rounds_worker(rank, world, port, run_ids, outdir):
+    import json
+    import random
+    from functools import partial
+
+    import torch.distributed as dist
+
+    from conftest import GOLDEN_DIR
+    from fedsim_amd.distributed.centralized import training
+    from fedsim_amd.sharding import ShardedSerialAggregator
+    from oracle import synthetic_fl as S
+    import shard_oracle
+    from shard_oracle import OracleEntry
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with open(os.path.join(GOLDEN_DIR, "rounds.json")) as f:
+            runs = {r["id"]: r for r in json.load(f)["runs"]}
+        for rid in run_ids:
+            run = runs[rid]
+            cls = S.make_algorithm(getattr(training, run["algorithm"]))
+            random.seed(S.RANDOM_SEED)
+            torch.manual_seed(S.TORCH_SEED)
+            alg = cls(data_manager=S.FakeDataManager(), metric_logger=None,
+                      num_clients=S.NUM_CLIENTS, sample_scheme="uniform",
+                      sample_rate=S.SAMPLE_RATE, model_def=S.TinyModel, epochs=1,
+                      criterion_def="CrossEntropyScore",
+                      optimizer_def=partial(torch.optim.SGD, **run["opt_kwargs"]),
+                      device="cpu",
+                      aggregator_factory=partial(ShardedSerialAggregator,
+                                                 entry_factory=OracleEntry),
+                      **run["alg_kwargs"])
+            scores = alg.train(rounds=S.ROUNDS)
+            st = alg.get_server_storage()
+            out = {}
+            for name in ("cloud_params", "avg_params", "h"):
+                try:
+                    t = st.read(name, silent=True)
+                except Exception:  # noqa: BLE001 - key absent for this algorithm
+                    continue
+                if isinstance(t, torch.Tensor):
+                    out[name] = t.detach().cpu().numpy()
+            np.savez(os.path.join(outdir, f"{rid}_rank{rank}.npz"), **out)
+            with open(os.path.join(outdir, f"{rid}_rank{rank}.json"), "w") as f:
+                json.dump({k: float(v) for k, v in scores.items()}, f)
+            with open(os.path.join(outdir, f"{rid}_rank{rank}_calls.json"), "w") as f:
+                json.dump(shard_oracle.CALLS, f)
+            shard_oracle.CALLS.update(add=0, pop_step=0)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_aggregator_round_loop_bitwise(world):
+    import json
+
+    from conftest import GOLDEN_DIR
+
+    with open(os.path.join(GOLDEN_DIR, "rounds.json")) as f:
+        runs = [r for r in json.load(f)["runs"]
+                if r.get("client", "synthetic") == "synthetic" and r["algorithm"] != "FedDF"]
+    ids = [r["id"] for r in runs]
+    assert {r["algorithm"] for r in runs} >= {"FedAvg", "AdaBest", "FedNova", "FedDyn"}
+    with np.load(os.path.join(GOLDEN_DIR, "rounds.npz"), allow_pickle=False) as z:
+        arrays = {k: z[k] for k in z.files}
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rounds_worker, args=(world, _free_port(), ids, d), nprocs=world,
+                           join=True, start_method="spawn")
+        for run in runs:
+            for r in range(world):
+                got = np.load(os.path.join(d, f"{run['id']}_rank{r}.npz"))
+                for name in ("cloud_params", "avg_params", "h"):
+                    key = f"{run['id']}/{'cloud' if name == 'cloud_params' else name}"
+                    if key not in arrays:
+                        continue
+                    np.testing.assert_array_equal(bits(got[name]), bits(arrays[key]),
+                                                  err_msg=f"{run['id']} rank {r} {name}")
+                with open(os.path.join(d, f"{run['id']}_rank{r}.json")) as f:
+                    assert json.load(f) == run["scores"], run["id"]
+                with open(os.path.join(d, f"{run['id']}_rank{r}_calls.json")) as f:
+                    calls = json.load(f)
+                # every rank reduced its own slice and ran the narrowed step
+                # once per round (5 rounds)
+                assert calls["pop_step"] == 5 and calls["add"] >= 5, (run["id"], calls)
