@@ -104,6 +104,16 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
          ctypes.c_int64, ctypes.c_void_p],
     ),
+    "fedagg_pack_segments_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p],
+    ),
+    "fedagg_unpack_row_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_void_p, ctypes.c_void_p],
+    ),
     "fedagg_finalize_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p,

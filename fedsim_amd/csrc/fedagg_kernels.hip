@@ -950,23 +950,138 @@ __global__ __launch_bounds__(kBlock) void k_adabest_sgd(const float* __restrict_
 }
 
 // D2D pack of one client vector into row r of a column-blocked slab: a
-// streaming copy (16 B per lane in, 16 B per lane out, both coalesced inside a
-// column block).  The DMA engines are slower than the CUs for HBM->HBM copies.
+// streaming copy in tiles of kPackU * 1024 columns per workgroup, kPackU
+// 16-B non-temporal loads in flight per lane before its 16-B non-temporal
+// stores (both coalesced inside a column block; C is a multiple of 4).  The
+// DMA engines are slower than the CUs for HBM->HBM copies.
+constexpr int kPackU = 4;
+
 __global__ __launch_bounds__(kBlock) void k_pack_row(const float* __restrict__ src,
                                                      int64_t P, float* __restrict__ Xb,
                                                      int64_t Kcap, int64_t C, int64_t r) {
+  constexpr int64_t kTile = int64_t(kBlock) * 4 * kPackU;
+  const int64_t nvec = P / 4;
+  const int64_t ntiles = (P + kTile - 1) / kTile;
+  const int64_t cvec = C / 4;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    f32x4 v[kPackU];
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u) {
+      const int64_t i = t * (kTile / 4) + int64_t(u) * kBlock + threadIdx.x;
+      if (i < nvec) v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src) + i);
+    }
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u) {
+      const int64_t i = t * (kTile / 4) + int64_t(u) * kBlock + threadIdx.x;
+      if (i < nvec) {
+        const int64_t b = i / cvec;
+        __builtin_nontemporal_store(v[u], reinterpret_cast<f32x4*>(Xb + (b * Kcap + r) * C) +
+                                              (i - b * cvec));
+      }
+    }
+  }
+  if (blockIdx.x == 0 && static_cast<int64_t>(threadIdx.x) < P - nvec * 4) {
+    const int64_t p = nvec * 4 + threadIdx.x;
+    Xb[((p / C) * Kcap + r) * C + p % C] = src[p];
+  }
+}
+
+inline int pack_grid(int64_t P) {
+  const int64_t tiles = (P + int64_t(kBlock) * 4 * kPackU - 1) / (int64_t(kBlock) * 4 * kPackU);
+  return static_cast<int>(tiles < 1 ? 1 : tiles < 8192 ? tiles : 8192);
+}
+
+// vectorize_module straight into a slab row: the concatenation of a model's
+// parameter tensors (segments: {src, first column, length}, sorted, tiling
+// [0, P)) written to row r of a column-blocked slab in one launch, in place of
+// torch.cat + clone + pack (fedsim/utils/convert_parameters.py:78-94).
+//
+// A workgroup owns a tile of kPackU * 1024 consecutive columns; each lane owns
+// kPackU quads of 4 columns (one 16-B non-temporal store each: C is a
+// multiple of 4, so a quad never straddles a column block).  The tile's first
+// segment is found once by binary search over the short, cache-resident
+// table; lanes walk forward from it.  All of a lane's loads are issued before
+// its stores.  A quad inside one segment loads 16 B when its source is 16-B
+// aligned (a model whose parameters are views of one vector: one segment),
+// else four 4-B loads; a quad across a segment boundary gathers per column.
+
+__device__ __forceinline__ int64_t pack_seg_of(const int64_t* __restrict__ segs, int64_t nseg,
+                                               int64_t p) {
+  int64_t lo = 0, hi = nseg - 1;  // last segment whose first column <= p
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (segs[3 * mid + 1] <= p) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_segments(const int64_t* __restrict__ segs,
+                                                          int64_t nseg, int64_t P,
+                                                          float* __restrict__ Xb, int64_t Kcap,
+                                                          int64_t C, int64_t r) {
+  constexpr int64_t kTile = int64_t(kBlock) * 4 * kPackU;
+  const int64_t ntiles = (P + kTile - 1) / kTile;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t t0 = t * kTile;
+    int64_t seg = pack_seg_of(segs, nseg, t0);
+    f32x4 v[kPackU];
+    int64_t pq[kPackU];
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u) {
+      const int64_t p = t0 + (int64_t(u) * kBlock + threadIdx.x) * 4;
+      pq[u] = p;
+      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (p >= P) continue;
+      while (seg + 1 < nseg && segs[3 * (seg + 1) + 1] <= p) ++seg;
+      const int64_t off = segs[3 * seg + 1];
+      const int64_t end = off + segs[3 * seg + 2];
+      const float* s = reinterpret_cast<const float*>(segs[3 * seg]) + (p - off);
+      if (p + 4 <= end) {
+        if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
+          v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s));
+        } else {
+          v[u] = f32x4{s[0], s[1], s[2], s[3]};
+        }
+      } else {  // the quad crosses a segment boundary, or P
+        int64_t sg = seg;
+        for (int j = 0; j < 4 && p + j < P; ++j) {
+          while (sg + 1 < nseg && segs[3 * (sg + 1) + 1] <= p + j) ++sg;
+          const int64_t o = segs[3 * sg + 1];
+          if (p + j < o + segs[3 * sg + 2])  // a table that does not tile [0, P)
+            v[u][j] = reinterpret_cast<const float*>(segs[3 * sg])[p + j - o];  // leaves 0
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u) {
+      const int64_t p = pq[u];
+      if (p >= P) continue;
+      float* dst = Xb + ((p / C) * Kcap + r) * C + p % C;
+      if (p + 4 <= P) {
+        __builtin_nontemporal_store(v[u], reinterpret_cast<f32x4*>(dst));
+      } else {
+        for (int j = 0; j < 4 && p + j < P; ++j) dst[j] = v[u][j];
+      }
+    }
+  }
+}
+
+// Row r of a column-blocked slab back to a contiguous vector (a slab row
+// handed out by vectorize_module, read as an ordinary tensor).
+__global__ __launch_bounds__(kBlock) void k_unpack_row(const float* __restrict__ Xb,
+                                                       int64_t Kcap, int64_t C, int64_t r,
+                                                       int64_t P, float* __restrict__ dst) {
   const int64_t nvec = P / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   const int64_t cvec = C / 4;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec; i += stride) {
     const int64_t b = i / cvec;
     const int64_t c = i - b * cvec;
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src) + i);
-    reinterpret_cast<f32x4*>(Xb + (b * Kcap + r) * C)[c] = v;
+    reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(Xb + (b * Kcap + r) * C)[c];
   }
   if (blockIdx.x == 0 && static_cast<int64_t>(threadIdx.x) < P - nvec * 4) {
     const int64_t p = nvec * 4 + threadIdx.x;
-    Xb[((p / C) * Kcap + r) * C + p % C] = src[p];
+    dst[p] = Xb[((p / C) * Kcap + r) * C + p % C];
   }
 }
 
@@ -1454,6 +1569,28 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   return static_cast<int>(e);
 }
 
+int fedagg_pack_segments_f32(const int64_t* segs, int64_t nseg, int64_t P, float* Xb,
+                             int64_t Kcap, int64_t C, int64_t r, void* stream) {
+  if (P < 0 || nseg < 0 || Kcap <= 0 || r < 0 || r >= Kcap) return FEDAGG_EINVAL;
+  if (C != 1024 && C != 2048 && C != 4096) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!segs || nseg == 0 || !Xb || !aligned16(Xb)) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_pack_segments, dim3(pack_grid(P)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), segs, nseg, P, Xb, Kcap, C, r);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_unpack_row_f32(const float* Xb, int64_t Kcap, int64_t C, int64_t r, int64_t P,
+                          float* dst, void* stream) {
+  if (P < 0 || Kcap <= 0 || r < 0 || r >= Kcap) return FEDAGG_EINVAL;
+  if (C != 1024 && C != 2048 && C != 4096) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!Xb || !dst || !aligned16(Xb) || !aligned16(dst)) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_unpack_row, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), Xb, Kcap, C, r, P, dst);
+  return static_cast<int>(hipGetLastError());
+}
+
 int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, int64_t C,
                         int64_t r, void* stream) {
   if (P < 0 || Kcap <= 0 || r < 0 || r >= Kcap) return FEDAGG_EINVAL;
@@ -1465,7 +1602,7 @@ int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, in
   if (hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeDevice &&
       aligned16(src) && aligned16(Xb)) {
     // HBM -> HBM: copy kernel on the CUs
-    hipLaunchKernelGGL(k_pack_row, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0, s, src,
+    hipLaunchKernelGGL(k_pack_row, dim3(pack_grid(P)), dim3(kBlock), 0, s, src,
                        P, Xb, Kcap, C, r);
     return static_cast<int>(hipGetLastError());
   }

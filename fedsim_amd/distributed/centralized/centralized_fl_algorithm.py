@@ -21,6 +21,7 @@ from torch.utils.data import DataLoader
 
 from ... import scores as _scores
 from ...utils import AppendixAggregator, SerialAggregator, Storage, apply_on_dict
+from ...utils.slab_rows import round_aggregator
 
 try:  # progress bar is cosmetic
     from tqdm import trange as _trange
@@ -226,13 +227,17 @@ class CentralFLAlgorithm(object):
             self._at_round_start()
             round_serial_aggregator = self._aggregator_factory()
             round_appendix_aggregator = AppendixAggregator()
-            for client_id in self._sample_clients():
-                client_msg = self._send_to_server(client_id)
-                success = self._receive_from_client(client_msg, round_serial_aggregator,
-                                                    round_appendix_aggregator)
-                if not success:
-                    diverged = True
-                    break
+            # clients that train on the GPU vectorize straight into this
+            # round's HBM slab (utils/slab_rows.py)
+            with round_aggregator(round_serial_aggregator):
+                for client_id in self._sample_clients():
+                    client_msg = self._send_to_server(client_id)
+                    success = self._receive_from_client(client_msg, round_serial_aggregator,
+                                                        round_appendix_aggregator)
+                    del client_msg  # the aggregator may hold the message's tensor
+                    if not success:
+                        diverged = True
+                        break
             if diverged:
                 # drop the round's slab without launching
                 del round_serial_aggregator

@@ -27,6 +27,7 @@ from torch.utils.data import DataLoader, RandomSampler
 
 from ....local import default_step_closure, local_inference, local_train
 from ....utils import vector_to_parameters_like, vectorize_module
+from ....utils.slab_rows import reserve_round_row
 
 
 def _grad_hook(coef_vec_fn):
@@ -76,8 +77,10 @@ def sgd_update(rounds, datasets, train_split_name, scores, epochs, criterion, tr
             model, DataLoader(split, batch_size=inference_batch_size, shuffle=False),
             scores[name], device=device)
         metrics[name] = _split_scores(scores, name)
-    return dict(local_params=vectorize_module(model), num_steps=n_steps, diverged=diverged,
-                num_samples=counts, metrics=metrics)
+    # on the GPU the update is written straight into the round's HBM slab
+    row = reserve_round_row("local_params", model)
+    return dict(local_params=vectorize_module(model, out=row), num_steps=n_steps,
+                diverged=diverged, num_samples=counts, metrics=metrics)
 
 
 def proximal_update(rounds, datasets, train_split_name, scores, epochs, criterion,

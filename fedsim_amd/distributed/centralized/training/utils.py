@@ -37,6 +37,7 @@ from .... import ops
 from ....local import local_inference
 from ....utils import initialize_module, vectorize_module
 from ....utils.aggregators import SerialAggregator as _DeviceSerialAggregator
+from ....utils.slab_rows import SlabRow
 
 
 def serial_aggregation(
@@ -106,6 +107,8 @@ def _handed_over(t: torch.Tensor) -> bool:
         return False
     if _refcount(t) > _OWNED_REFS:
         return False
+    if isinstance(t, SlabRow):  # a reserved slab row: no storage of its own
+        return True
     # one TensorImpl + the temporary storage object created here
     return torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= 2
 

@@ -296,6 +296,88 @@ def pack_row(src: torch.Tensor, Xb: torch.Tensor, r: int, stream=None) -> None:
     check(rc, "fedagg_pack_row_f32")
 
 
+def segments(tensors: Sequence[torch.Tensor], device: torch.device):
+    """([[pointer, first column, length], ...], P): the segments that
+    concatenate ``tensors`` (fedagg_pack_segments_f32).  Adjacent tensors that
+    are adjacent in memory -- a model's parameters after
+    ``vector_to_parameters`` made them views of one vector -- are one segment.
+    Every tensor must be a contiguous fp32 tensor on ``device``."""
+    segs = []
+    P = 0
+    for i, t in enumerate(tensors):
+        if t.dtype != torch.float32 or t.device != device or not t.is_contiguous():
+            raise ValueError(f"tensors[{i}] must be a contiguous float32 tensor on {device}")
+        n = t.numel()
+        if n == 0:
+            continue
+        ptr = t.data_ptr()
+        if segs and segs[-1][0] + 4 * segs[-1][2] == ptr:
+            segs[-1][2] += n
+        else:
+            segs.append([ptr, P, n])
+        P += n
+    return segs, P
+
+
+_TABLES: dict = {}  # (device, segments) -> device table; a model's layout repeats
+
+
+def segment_table(tensors: Sequence[torch.Tensor], device: torch.device):
+    """(device int64 table, number of segments, P) for fedagg_pack_segments_f32."""
+    segs, P = segments(tensors, device)
+    key = (device, tuple(v for seg in segs for v in seg))
+    table = _TABLES.get(key)
+    if table is None:
+        if len(_TABLES) > 64:
+            _TABLES.clear()
+        host = torch.tensor(list(key[1]) or [0, 0, 0], dtype=torch.int64).pin_memory()
+        table = _TABLES[key] = host.to(device, non_blocking=True)
+    return table, len(segs), P
+
+
+def pack_segments(tensors: Sequence[torch.Tensor], Xb: torch.Tensor, r: int) -> int:
+    """Write the concatenation of ``tensors`` (a model's parameters, in order)
+    into row ``r`` of the column-blocked slab ``Xb`` in one launch:
+    vectorize_module straight into the slab.  One segment (parameters that are
+    views of one vector, as a round's client models are) is the plain row
+    pack (fedagg_pack_row_f32); several go through a device table of segments
+    (fedagg_pack_segments_f32, tables cached per layout).  Returns P."""
+    _require_hip_f32(Xb, "Xb")
+    nb, Kcap, C = Xb.shape
+    segs, P = segments(tensors, Xb.device)
+    if nb != (P + C - 1) // C or not 0 <= r < Kcap:
+        raise ValueError("tensors / slab shape mismatch")
+    lib = _native.load()
+    if len(segs) == 1 and segs[0][0] % 16 == 0:
+        rc = lib.fedagg_pack_row_f32(segs[0][0], P, Xb.data_ptr(), Kcap, C, r,
+                                     _stream_ptr(Xb.device))
+        check(rc, "fedagg_pack_row_f32")
+        return P
+    table, nseg, _ = segment_table(tensors, Xb.device)
+    rc = lib.fedagg_pack_segments_f32(table.data_ptr(), nseg, P, Xb.data_ptr(), Kcap, C, r,
+                                      _stream_ptr(Xb.device))
+    check(rc, "fedagg_pack_segments_f32")
+    return P
+
+
+def unpack_row(Xb: torch.Tensor, r: int, P: int, out: Optional[torch.Tensor] = None):
+    """Row ``r`` of a column-blocked slab as a contiguous [P] vector
+    (fedagg_unpack_row_f32)."""
+    _require_hip_f32(Xb, "Xb")
+    nb, Kcap, C = Xb.shape
+    if nb != (P + C - 1) // C or not 0 <= r < Kcap:
+        raise ValueError("slab / row mismatch")
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=Xb.device)
+    _require_hip_f32(out, "out")
+    if out.numel() != P or not out.is_contiguous() or out.device != Xb.device:
+        raise ValueError(f"out must be a contiguous [{P}] tensor on {Xb.device}")
+    rc = _native.load().fedagg_unpack_row_f32(Xb.data_ptr(), Kcap, C, r, P, out.data_ptr(),
+                                              _stream_ptr(Xb.device))
+    check(rc, "fedagg_unpack_row_f32")
+    return out
+
+
 def finalize(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = fl32(acc / fl32(W)) — SerialAggregator.pop's true division."""
     _require_hip_f32(acc, "acc")

@@ -306,6 +306,11 @@ class ShardedSerialAggregator(SerialAggregator):
     def _new_entry(self, value: torch.Tensor) -> _TensorEntry:
         return _ShardEntry(self, value)
 
+    def reserve(self, key, P, device):
+        """Client rows are not reserved in a sharded round (each rank keeps a
+        column slice of every vector, not whole rows)."""
+        return None
+
     @property
     def rank(self) -> int:
         return self._rank

@@ -37,6 +37,7 @@ import torch
 
 from .. import ops
 from .dict_ops import apply_on_dict
+from .slab_rows import RowRefs, SlabRow
 
 __all__ = ["SerialAggregator", "DeviceAggregator", "AppendixAggregator"]
 
@@ -143,6 +144,20 @@ def _ingest_for(dev: torch.device) -> _Ingest:
     return ing
 
 
+class _Like(object):
+    """Shape / size / device of a key's vectors before any value arrives."""
+
+    def __init__(self, shape, device):
+        self.shape = shape
+        self.device = device
+        self._n = 1
+        for d in shape:
+            self._n *= d
+
+    def numel(self):
+        return self._n
+
+
 class _Options(object):
     __slots__ = ("device", "slab_bytes", "max_rows", "flags", "expected_rows", "block_cols",
                  "borrow", "fast")
@@ -206,12 +221,15 @@ class _DeviceEntry(_TensorEntry):
         self.pending_w: List[float] = []
         self.acc: Optional[torch.Tensor] = None
         self.cur_w = 0
+        self.rows = RowRefs()        # SlabRows handed out by reserve()
         self.copy_event = None       # last host DMA into the slab (copy stream)
         self.last_flush_event = None  # last reduction reading the slab (compute stream)
         self.wait_before_copy = None
 
     # -- ring management -----------------------------------------------------
     def _alloc(self, rows: int) -> None:
+        if self.slab is not None:
+            self.rows.release(self.slab)
         self.slab = torch.empty((self.nblk, rows, self.C), dtype=torch.float32, device=self.dev)
         self.R = rows
         self.head = self.tail = 0
@@ -232,6 +250,32 @@ class _DeviceEntry(_TensorEntry):
             # double buffering: drain one half while the other half fills
             self._flush(final_W=None)
 
+    def _claim(self, r: int) -> None:
+        """Row r is about to be written: a live SlabRow still showing it is
+        copied out first, and the next host DMA waits for that copy."""
+        if self.rows.claim(r, self.slab):
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            self.wait_before_copy = ev
+
+    def reserve(self) -> SlabRow:
+        """The next ring row, as a SlabRow a client can vectorize its model
+        into (slab_rows.py); ``add`` of that row commits it in place."""
+        if self.borrowed:
+            self._flush(final_W=None)  # earlier borrowed rows first: arrival order
+        self._make_room()
+        r = self.head
+        self._claim(r)
+        row = SlabRow(self, self.slab, r, self.P)
+        self.rows.track(row)
+        return row
+
+    def release(self) -> None:
+        """Drop the slab; SlabRows still alive keep a copy of their row."""
+        if self.slab is not None:
+            self.rows.release(self.slab)
+        self.slab = None
+
     # -- reference semantics -------------------------------------------------
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
@@ -246,6 +290,20 @@ class _DeviceEntry(_TensorEntry):
         # taken as is: detach / reshape allocate a new tensor object each,
         # a few us per client on the host
         src = value.detach() if value.requires_grad else value
+        if isinstance(src, SlabRow):
+            if (src._entry is self and src.in_slab and src._slab is self.slab
+                    and src._row == self.head and not src._committed):
+                # the client wrote its vector into the row reserved for it:
+                # commit in place (vectorize_module(..., out=reserve()))
+                if self.borrowed:
+                    self._flush(final_W=None)
+                src._committed = True
+                self.head = (self.head + 1) % self.R
+                self.n_pending += 1
+                self.pending_w.append(w32)
+                self.cur_w = new_w
+                return
+            src = src.materialize()  # another entry's row, or a stale one
         if src.dim() != 1:
             src = src.reshape(-1)
         if self.borrow and self._borrowable(src):
@@ -261,6 +319,7 @@ class _DeviceEntry(_TensorEntry):
             self._flush(final_W=None)
         self._make_room()
         r = self.head
+        self._claim(r)
         if src.device.type == "cuda":
             if src.device != self.dev:
                 src = src.to(self.dev)
@@ -375,7 +434,7 @@ class _DeviceEntry(_TensorEntry):
     def pop(self, on_device: bool = False) -> torch.Tensor:
         self._flush(final_W=self.cur_w if self._weighted() else None)
         out = self.acc.view(self.shape) if on_device else self._deliver(self.acc)
-        self.slab = None
+        self.release()
         self.acc = None
         return out
 
@@ -393,7 +452,7 @@ class _DeviceEntry(_TensorEntry):
             step.apply(self.pop(on_device=True).reshape(-1))
             return
         self._flush(final_W=self.cur_w if self._weighted() else None, step=step)
-        self.slab = None
+        self.release()
         self.acc = None
 
 
@@ -431,6 +490,7 @@ class SerialAggregator(object):
                  block_cols: Optional[int] = None, borrow: bool = False,
                  fast: bool = False) -> None:
         self._members: Dict = dict()
+        self._reserved: Dict = dict()  # keys with reserved rows but no add yet
         self._opts = _Options(device, slab_bytes, max_rows, flags, expected_rows, block_cols,
                               borrow, fast)
     @staticmethod
@@ -445,8 +505,28 @@ class SerialAggregator(object):
     def _is_device_value(value) -> bool:
         return isinstance(value, torch.Tensor) and value.dim() > 0
 
+    def reserve(self, key, P: int, device) -> Optional[SlabRow]:
+        """A row of ``key``'s HBM ring for a client to write its P-parameter
+        vector into (slab_rows.reserve_round_row / vectorize_module(out=)),
+        or None if this key cannot take one (not part of the reference API).
+        The key does not exist for ``in`` / ``pop_all`` until a value is
+        added."""
+        e = self._members.get(key)
+        if e is None:
+            e = self._reserved.get(key)
+        if e is None:
+            like = _Like((P,), torch.device(device))
+            e = _DeviceEntry(like, _hip_device(like, self._opts.device), self._opts, self)
+            self._reserved[key] = e
+        if type(e) is not _DeviceEntry or e.P != P or e.dev != torch.device(device) \
+                or e.shape != (P,):
+            return None
+        return e.reserve()
+
     def add(self, key, value, weight=None):
         entry = self._members.get(key)
+        if entry is None and key in self._reserved and self._is_device_value(value):
+            entry = self._members[key] = self._reserved.pop(key)
         if isinstance(entry, _TensorEntry):
             if not self._is_device_value(value):
                 raise TypeError(f"key {key!r} aggregates tensors; got {type(value).__name__}")

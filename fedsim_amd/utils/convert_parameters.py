@@ -8,6 +8,8 @@ from collections import OrderedDict
 
 import torch
 from torch import Tensor
+
+from .. import ops
 from torch.nn import Module
 from torch.nn.utils import parameters_to_vector, vector_to_parameters
 
@@ -35,10 +37,30 @@ def vector_to_named_parameters_like(vec: Tensor, named_parameters_like) -> Order
     return out
 
 
-def vectorize_module(module: Module, clone=True, detach=True) -> Tensor:
+def vectorize_module(module: Module, clone=True, detach=True, out=None) -> Tensor:
+    """``module``'s parameters as one flat vector (reference:
+    fedsim/utils/convert_parameters.py:78-94).
+
+    The reference's ``clone`` is a second copy of what ``parameters_to_vector``
+    (``torch.cat``) has just written to fresh memory: the result already
+    shares nothing with the parameters, so the copy is skipped and the
+    returned vector is the same either way.
+
+    ``out``: a reserved slab row (slab_rows.SlabRow, from
+    ``slab_rows.reserve_round_row``): the parameters are written straight into
+    it (fedagg_pack_segments_f32, one launch) and the row is returned."""
+    if out is not None:
+        from .slab_rows import SlabRow
+
+        if not isinstance(out, SlabRow) or not out.in_slab:
+            raise TypeError("out must be a reserved SlabRow still in its slab")
+        params = [p.detach() for p in module.parameters()]
+        P = sum(p.numel() for p in params)
+        if P != out.shape[0]:
+            raise ValueError(f"module has {P} parameters, the row {out.shape[0]}")
+        ops.pack_segments(params, out._slab, out._row)
+        return out
     vec = parameters_to_vector(module.parameters())
-    if clone:
-        vec = vec.clone()
     if detach:
         vec = vec.detach()
     return vec

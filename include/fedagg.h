@@ -167,6 +167,26 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
                               float W32, int flags, void* stream);
 
 /*
+ * vectorize_module straight into a slab row (fedsim/utils/convert_parameters.py
+ * :78-94, parameters_to_vector + the clone at training/utils.py:34): write
+ * the concatenation of nseg device segments into row r of a column-blocked
+ * slab [ceil(P/C), Kcap, C] in one launch.  segs is a DEVICE array of nseg
+ * int64 triples {source pointer, first column, length > 0}, sorted by first
+ * column and tiling [0, P) exactly (a model's parameters in registration
+ * order; adjacent parameters that are adjacent in memory may be one segment).
+ * Xb must be 16-byte aligned.
+ */
+int fedagg_pack_segments_f32(const int64_t* segs, int64_t nseg, int64_t P, float* Xb,
+                             int64_t Kcap, int64_t C, int64_t r, void* stream);
+
+/*
+ * Row r of a column-blocked slab copied out to P contiguous fp32 at dst (both
+ * 16-byte aligned device memory): a slab row read back as a flat vector.
+ */
+int fedagg_unpack_row_f32(const float* Xb, int64_t Kcap, int64_t C, int64_t r, int64_t P,
+                          float* dst, void* stream);
+
+/*
  * Pack one client vector (P contiguous fp32, host-pinned or device memory)
  * into row r of a column-blocked slab [ceil(P/C), Kcap, C] with one 2-D DMA.
  * This is the HBM side of SerialAggregator.add's snapshot (the reference's
