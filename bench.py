@@ -87,6 +87,10 @@ def parse(argv=None):
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--master-port", type=int, default=0,
                     help="rendezvous port of the self-spawned ranks (0: pick a free one)")
+    ap.add_argument("--one-gpu-rehearsal", action="store_true",
+                    help="TEST ONLY: every rank on cuda:0 over a gloo group, to rehearse "
+                         "the N-rank launcher with the HIP kernels on a one-GPU box (ranks "
+                         "share the GPU: the value is not a scaling number)")
     ap.add_argument("--rehearsal-stub", default=None, metavar="MODULE:FN",
                     help="TEST ONLY: run the launcher and the collectives on CPU over gloo, "
                          "with the per-rank reduction done by MODULE:FN (no GPU, no HIP "
@@ -210,6 +214,7 @@ class Rank(object):
             self.stub = getattr(importlib.import_module(mod), fn)
             self.dev = torch.device("cpu")
         else:
+            self.local = 0 if a.one_gpu_rehearsal else self.local
             torch.cuda.set_device(self.local)
             self.dev = torch.device("cuda", self.local)
         # any torch.distributed.run launch (even --nproc-per-node 1) takes the
@@ -218,7 +223,7 @@ class Rank(object):
         if self.world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ):
             import torch.distributed as dist
 
-            if self.rehearsal:
+            if self.rehearsal or a.one_gpu_rehearsal:
                 dist.init_process_group("gloo")
             else:
                 dist.init_process_group(backend="nccl", device_id=self.dev)
@@ -667,6 +672,9 @@ def _main(a, quiet):
         result["rehearsal"] = "cpu/gloo launcher rehearsal, per-rank reduce = " + a.rehearsal_stub
         result["roofline"] = None
     else:
+        if a.one_gpu_rehearsal:
+            result["rehearsal"] = ("one-GPU launcher rehearsal: %d ranks share cuda:0 over "
+                                   "gloo (not a scaling number)" % rk.world)
         result["world_size_seen"] = rk.dist.get_world_size() if rk.dist is not None else 1
         result["backend"] = rk.dist.get_backend() if rk.dist is not None else None
         achieved = nbytes / (kern_ms_max * 1e-3) / 1e9

@@ -527,6 +527,7 @@ class SerialAggregator(object):
         entry = self._members.get(key)
         if entry is None and key in self._reserved and self._is_device_value(value):
             entry = self._members[key] = self._reserved.pop(key)
+            entry.out_device = value.device  # results go where the first value came from
         if isinstance(entry, _TensorEntry):
             if not self._is_device_value(value):
                 raise TypeError(f"key {key!r} aggregates tensors; got {type(value).__name__}")

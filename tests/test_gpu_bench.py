@@ -1,0 +1,37 @@
+"""bench.py's own N-rank launcher with the HIP kernels: two ranks started by
+``bench.py --gpus 2`` itself, both on the one GPU of the box over a gloo group
+(``--one-gpu-rehearsal``; the 8-GPU RCCL run is the driver's), every mode:
+exactly one JSON line on stdout with n_gpus 2, the world size the ranks saw,
+and a roofline measured by each rank's HIP events."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("mode,extra", [
+    ("param", ["--K", "64", "--P", "2000000"]),
+    ("strong", ["--K", "300", "--P", "2000000", "--pool-rows", "128"]),
+    ("allreduce", ["--K", "300", "--P", "2000000", "--pool-rows", "128"]),
+])
+def test_launcher_two_ranks_one_gpu(mode, extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--mode",
+                        mode, "--one-gpu-rehearsal", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", *extra],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size_seen"] == 2 and d["backend"] == "gloo"
+    assert d["roofline"]["achieved"] > 0 and d["roofline"]["launch_ms"] > 0
+    assert "rehearsal" in d
+    if mode == "allreduce":
+        assert d["allreduce"]["ms"] is not None
