@@ -249,6 +249,94 @@ class _ShardEntry(_TensorEntry):
             self._gather_into(t, None)
 
 
+class _DevicesEntry(_TensorEntry):
+    """One tensor key of a single-process ShardedSerialAggregator over
+    several local GPUs: shard i (columns [lo_i, hi_i)) is reduced by a
+    one-GPU entry on devices[i]; results are assembled by copies between the
+    devices (or into one pinned host tensor)."""
+
+    def __init__(self, agg: "ShardedSerialAggregator", value: torch.Tensor):
+        self.agg = agg
+        self.shape = tuple(value.shape)
+        self.P = value.numel()
+        self.out_device = value.device
+        n = len(agg._devices)
+        self.spans = [shard_span(self.P, i, n) for i in range(n)]
+        flat = value.reshape(-1)
+        self.inners = [None if hi <= lo else
+                       _DeviceEntry(flat[lo:hi], dev, agg._opts, agg, out_device=dev)
+                       for (lo, hi), dev in zip(self.spans, agg._devices)]
+        self.cur_w = 0
+
+    @property
+    def dev(self):
+        """Where the server step's operands should live: with the results
+        (the host for a host-resident run: each GPU then moves only its
+        slice over its own link)."""
+        return self.out_device
+
+    def add(self, value: torch.Tensor, weight) -> None:
+        new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
+        if tuple(value.shape) != self.shape:
+            raise ValueError(
+                f"tensor of shape {tuple(value.shape)} added to a key aggregating {self.shape}")
+        src = value.detach() if value.requires_grad else value
+        flat = src.reshape(-1)
+        for (lo, hi), inner in zip(self.spans, self.inners):
+            if inner is not None:
+                inner.add(flat[lo:hi], weight)  # host slices: each GPU's own copy stream
+        self.cur_w = new_w
+
+    def _assemble(self, parts, on=None) -> torch.Tensor:
+        on = self.out_device if on is None else on
+        host = on.type == "cpu"
+        full = torch.empty(self.P, dtype=torch.float32, device=on, pin_memory=host)
+        for (lo, hi), part in zip(self.spans, parts):
+            if part is not None:
+                full[lo:hi].copy_(part.reshape(-1), non_blocking=host)
+        if host:
+            for inner in self.inners:
+                if inner is not None:
+                    torch.cuda.current_stream(inner.dev).synchronize()
+        return full
+
+    def get(self) -> torch.Tensor:
+        return self._assemble([None if e is None else e.get() for e in self.inners]).view(
+            self.shape)
+
+    def get_sum(self) -> torch.Tensor:
+        return self._assemble([None if e is None else e.get_sum() for e in self.inners]).view(
+            self.shape)
+
+    def pop(self, on_device: bool = False) -> torch.Tensor:
+        parts = [None if e is None else e.pop(on_device=True) for e in self.inners]
+        return self._assemble(parts).view(self.shape)
+
+    def pop_step(self, step: ops.ServerStep) -> None:
+        """Each GPU runs the step on its slice: in place when the operands
+        live on that GPU, else on a copy of the operand slices moved over
+        that GPU's own link (PCIe for a host-resident cloud), copied back."""
+        home = step.cloud.device
+        back = []
+        for (lo, hi), inner in zip(self.spans, self.inners):
+            if inner is None:
+                continue
+            sub = step.narrow(lo, hi)
+            if inner.dev != home:
+                moved = {n: t.to(inner.dev, non_blocking=True) for n, t in sub.operands.items()}
+                local = ops.ServerStep(step.algo, moved.pop("cloud"), **step._scalars, **moved)
+                inner.pop_step(local)
+                back.append((sub, local, inner.dev))
+            else:
+                inner.pop_step(sub)
+        for sub, local, dev in back:
+            host = home.type == "cpu"
+            for name, t in local.operands.items():
+                sub.operands[name].copy_(t, non_blocking=host)
+            if host:
+                torch.cuda.current_stream(dev).synchronize()
+
+
 class ShardedSerialAggregator(SerialAggregator):
     """Parameter-sharded drop-in for the reference SerialAggregator
     (fedsim/utils/aggregators.py:11-144) over the ranks of a process group,
@@ -277,19 +365,38 @@ class ShardedSerialAggregator(SerialAggregator):
     Scalar keys (the per-split metrics) stay on the host with the
     reference's arithmetic, identically on every rank.
 
+    Single-process mode (``devices=[...]``): one process drives several
+    local GPUs, shard i on devices[i] -- for FedSim's own single-process
+    simulator.  Host client vectors cross PCIe slice by slice, one link per
+    GPU; the server step runs on each GPU's slice of the cloud (moved over
+    that GPU's link when the cloud lives on the host) and the results are
+    assembled in one pinned host tensor (or on the cloud's GPU).  HBM
+    vectors of one GPU reach the other shards over xGMI.
+
     Args:
         group: the torch.distributed group (default: the default group; a
             single process with no group is world 1).
+        devices: single-process mode (see above); excludes ``group``.
         entry_factory: TEST HOOK.  ``entry_factory(slice, agg)`` builds the
             per-rank state of a key instead of the HIP entry, so the protocol
             can be rehearsed with gloo on CPU (tests/test_sharding_gloo.py).
         **kwargs: SerialAggregator's options, applied to each rank's slice.
     """
 
-    def __init__(self, group=None, entry_factory: Optional[Callable] = None, **kwargs) -> None:
+    def __init__(self, group=None, entry_factory: Optional[Callable] = None,
+                 devices: Optional[Sequence] = None, **kwargs) -> None:
         super().__init__(**kwargs)
-        self._group = group
-        self._rank, self._world = _group_rank_world(group)
+        self._devices = None
+        if devices is not None:
+            if group is not None or entry_factory is not None:
+                raise ValueError("devices= is the single-process mode: no group / entry_factory")
+            self._devices = [torch.device(d) for d in devices]
+            if not self._devices or any(d.type != "cuda" for d in self._devices):
+                raise ValueError("devices must be one or more HIP devices")
+            self._group, self._rank, self._world = None, 0, 1
+        else:
+            self._group = group
+            self._rank, self._world = _group_rank_world(group)
         self._entry_factory = entry_factory
 
     def _device_for(self, value: torch.Tensor) -> torch.device:
@@ -304,6 +411,8 @@ class ShardedSerialAggregator(SerialAggregator):
         return _DeviceEntry(part, dev, self._opts, self, out_device=dev)
 
     def _new_entry(self, value: torch.Tensor) -> _TensorEntry:
+        if self._devices is not None:
+            return _DevicesEntry(self, value)
         return _ShardEntry(self, value)
 
     def reserve(self, key, P, device):
