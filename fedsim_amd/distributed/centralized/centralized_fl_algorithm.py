@@ -60,6 +60,7 @@ class CentralFLAlgorithm(object):
         device="cpu",
         *args,
         aggregator_factory=None,
+        shard_over=None,
         progress=False,
         **kwargs,
     ):
@@ -101,14 +102,26 @@ class CentralFLAlgorithm(object):
         # size each round's HBM ring once for the clients it will receive, and
         # reduce HBM-resident client vectors in place: a message is dropped
         # right after receive_from_client, so its tensor can be handed over.
-        # Under a torch.distributed group of several ranks (one process per
-        # GPU, every rank running this same round loop) each rank reduces and
-        # steps its own column shard of the model (fedsim_amd.sharding).
+        # shard_over (not in the reference): spread each round's aggregation
+        # over several GPUs by columns (fedsim_amd.sharding) -- "group" (the
+        # default torch.distributed group: every rank runs this same round
+        # loop, one process per GPU), a ProcessGroup, or a list of local
+        # devices (one process driving several GPUs).  Opt-in: ranks of a
+        # group that run different simulations must not be sharded together.
         if aggregator_factory is None:
-            cls = SerialAggregator
-            if _distributed_world() > 1:
-                from ...sharding import ShardedSerialAggregator as cls
-            aggregator_factory = partial(cls, expected_rows=sample_count, borrow=True)
+            kw = dict(expected_rows=sample_count, borrow=True)
+            if shard_over is None:
+                aggregator_factory = partial(SerialAggregator, **kw)
+            else:
+                from ...sharding import ShardedSerialAggregator
+
+                if isinstance(shard_over, (list, tuple)):
+                    kw["devices"] = list(shard_over)
+                elif shard_over != "group":
+                    kw["group"] = shard_over
+                aggregator_factory = partial(ShardedSerialAggregator, **kw)
+        elif shard_over is not None:
+            raise ValueError("pass either aggregator_factory or shard_over")
         self._aggregator_factory = aggregator_factory
         self._progress = progress
         self._server_memory = Storage()
