@@ -51,7 +51,7 @@ def serial_aggregation(
     purge_msg=True,
 ):
     params = client_msg["local_params"]
-    if not _handed_over(params) and _would_borrow(aggregator, params):
+    if _would_borrow(aggregator, params) and not _handed_over(params):
         params = params.clone()  # the reference's snapshot (utils.py:34)
     if params.requires_grad:  # detach only when needed: it allocates a tensor object
         params = params.detach()

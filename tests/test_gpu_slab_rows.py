@@ -219,3 +219,41 @@ def test_round_loop_local_sgd_same_bits_with_slab_rows(rid):
         outs.append((st.read("cloud_params").detach().cpu().numpy(), scores))
     np.testing.assert_array_equal(bits(outs[0][0]), bits(outs[1][0]))
     assert outs[0][1] == outs[1][1]
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_pack_segments_random_layouts(seed):
+    """Random parameter layouts: ragged sizes, views at unaligned offsets of
+    one buffer (16-B and 4-B load paths, quads across segment boundaries),
+    adjacent views that merge into one segment, every block width and row;
+    the packed row reads back as torch.cat of the tensors, and no other row
+    of the slab is touched."""
+    from fedsim_amd import ops
+
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 10))
+    big = torch.randn(400_000, device=DEV)
+    tensors, pos = [], int(rng.integers(0, 7))
+    for i in range(n):
+        size = int(rng.choice([1, 2, 3, 5, 4, 64, 1000, 4097, int(rng.integers(1, 60_000))]))
+        if rng.random() < 0.5:  # a view of the shared buffer, maybe right after the last
+            if rng.random() < 0.5:
+                pos += int(rng.integers(0, 9))
+            if pos + size > big.numel():
+                pos = 0
+            tensors.append(big[pos:pos + size])
+            pos += size
+        else:
+            tensors.append(torch.randn(size, device=DEV))
+    want = torch.cat(tensors)
+    P = want.numel()
+    C = int(rng.choice([1024, 2048, 4096]))
+    Kcap = int(rng.integers(1, 5))
+    r = int(rng.integers(0, Kcap))
+    Xb = torch.full(ops.blocked_shape(Kcap, P, C), float("nan"), device=DEV)
+    assert ops.pack_segments(tensors, Xb, r) == P
+    got = ops.unpack_row(Xb, r, P)
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+    others = [k for k in range(Kcap) if k != r]
+    if others:
+        assert torch.isnan(Xb[:, others, :]).all()

@@ -186,6 +186,12 @@ def main():
             res[name] = headline_round(K, P, dev, mode, a.reps, ragged)
             print(json.dumps({"headline_" + name: res[name]}), flush=True)
         print(json.dumps({"headline": res}), flush=True)
+        # the reference's own model sizes through the same GPU-client round
+        for name, (K, P) in CONFIGS.items():
+            res = dict(K=K, P=P)
+            for mode in ("slab_rows", "borrow_vector"):
+                res[mode] = headline_round(K, P, dev, mode, max(a.reps, 5))
+            print(json.dumps({"gpu_clients_" + name: res}), flush=True)
         if a.only == "headline":
             return
     names = [n for n in CONFIGS if not a.only or n in a.only.split(",")]

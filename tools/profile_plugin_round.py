@@ -13,7 +13,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from bench_plugin_round import messages, one_round  # noqa: E402
+from bench_plugin_round import headline_round, messages, one_round  # noqa: E402
 
 
 def main():
@@ -22,19 +22,27 @@ def main():
     ap.add_argument("--P", type=int, default=1_085_668)
     ap.add_argument("--borrow", type=int, default=1)
     ap.add_argument("--where", default=None,
-                    help="device_borrow | device_snap | host_pinned | host_pageable | cpu_run")
+                    help="device_borrow | device_snap | host_pinned | host_pageable | cpu_run "
+                         "| gpu_clients")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     where = a.where or ("device_borrow" if a.borrow else "device_snap")
-    msgs = messages(a.K, a.P, where, dev)
-    cloud = torch.zeros(a.P, device="cpu" if where == "cpu_run" else dev, requires_grad=True)
-    for _ in range(2):
-        one_round(msgs, cloud, bool(a.borrow))
     pr = cProfile.Profile()
-    pr.enable()
-    for _ in range(3):
-        one_round(msgs, cloud, bool(a.borrow))
-    pr.disable()
+    if where == "gpu_clients":  # vectorize into slab rows (bench_plugin_round.headline_round)
+        headline_round(a.K, a.P, dev, "slab_rows", 1)
+        pr.enable()
+        headline_round(a.K, a.P, dev, "slab_rows", 2)
+        pr.disable()
+    else:
+        cloud = torch.zeros(a.P, device="cpu" if where == "cpu_run" else dev,
+                            requires_grad=True)
+        for _ in range(2):  # one_round consumes its messages
+            one_round(messages(a.K, a.P, where, dev), cloud, bool(a.borrow))
+        batches = [messages(a.K, a.P, where, dev) for _ in range(3)]
+        pr.enable()
+        for msgs in batches:
+            one_round(msgs, cloud, bool(a.borrow))
+        pr.disable()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
     print(s.getvalue())
