@@ -20,6 +20,13 @@ MI355X-first differences (same results):
   average is one launch of the exact-mode reduce kernel
   (``fedagg_reduce_f32``, weights 1, divide by fl32(K)): the same per-element
   arithmetic and order as the reference's ``add(target, 1)`` x K + ``get``.
+* The teachers are fixed for the whole distillation (they are this round's
+  client models) and the server's dataloaders do not shuffle, so the
+  ensemble's mean logits of each batch are computed in the first epoch and
+  reused by the later ones (``global_epochs`` > 1) when the model's forward
+  is pure (no buffers to update, no dropout): the same batches, the same
+  forwards, the same bits, one teacher pass per round instead of one per
+  epoch.
 * Elsewhere (host-resident model, or a model with buffers such as BatchNorm,
   whose running statistics cannot be updated under vmap) the teachers run one
   after another, as in the reference, and their logits go through the
@@ -40,6 +47,26 @@ from .fedavg import FedAvg
 from .utils import serial_aggregation
 
 _TEACHER_CHUNK = 64  # teachers per batched forward (bounds activation memory)
+
+
+def _in_order(loader) -> bool:
+    """Whether iterating ``loader`` yields the same batches every time (no
+    shuffling or random sampling): then per-sample targets can be reused."""
+    from torch.utils.data import BatchSampler, SequentialSampler
+
+    bs = getattr(loader, "batch_sampler", None)
+    return isinstance(bs, BatchSampler) and isinstance(bs.sampler, SequentialSampler)
+
+
+def _pure_forward(model) -> bool:
+    """A forward with no side effects and no randomness: no buffers (e.g.
+    BatchNorm running statistics, updated by every reference forward in train
+    mode) and no dropout in train mode.  Only then may a teacher's output be
+    reused instead of recomputed as the reference does."""
+    if any(True for _ in model.buffers()):
+        return False
+    return not any(isinstance(m, torch.nn.modules.dropout._DropoutNd) and m.training
+                   for m in model.modules())
 
 
 class TeacherEnsemble(object):
@@ -118,11 +145,20 @@ class FedDF(FedAvg):
 
             teachers = TeacherEnsemble(model, appendix_aggregator.get_values("local_params"),
                                        device)
+            # the same batches every epoch: mean logits computed once, reused
+            cache = [] if (global_epochs > 1 and _in_order(train_data_loader)
+                           and _pure_forward(model)) else None
             ran = False
             for _ in range(global_epochs):
-                for x, _ in train_data_loader:
+                for j, (x, _) in enumerate(train_data_loader):
                     x = x.to(device)
-                    target_out = log_softmax(teachers.mean_logits(x), 1)
+                    if cache is not None and j < len(cache):
+                        logits = cache[j]
+                    else:
+                        logits = teachers.mean_logits(x)
+                        if cache is not None:
+                            cache.append(logits)
+                    target_out = log_softmax(logits, 1)
                     criterion = KLDivScore(log_target=True)
                     param_dict = vector_to_named_parameters_like(cloud_params,
                                                                  model.named_parameters())
