@@ -329,3 +329,24 @@ def test_weight_rounding_matches_aten():
     for v in vals:
         assert _fl32(v) == float(np.float32(float(v))), v
         assert _fl32(v) == float(torch.tensor(float(v), dtype=torch.float32)), v
+
+
+def test_feddf_target_reuse_conditions():
+    """FedDF reuses a batch's ensemble targets across global epochs only for
+    an in-order loader and a pure forward (no buffers, no train-mode dropout),
+    where recomputing them, as the reference does, gives the same values."""
+    import torch
+    from torch import nn
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from fedsim_amd.distributed.centralized.training.feddf import _in_order, _pure_forward
+
+    ds = TensorDataset(torch.zeros(10, 2), torch.zeros(10))
+    assert _in_order(DataLoader(ds, batch_size=4))
+    assert not _in_order(DataLoader(ds, batch_size=4, shuffle=True))
+    assert _pure_forward(nn.Sequential(nn.Linear(2, 3), nn.ReLU(), nn.Linear(3, 2)))
+    assert not _pure_forward(nn.Sequential(nn.Linear(2, 3), nn.BatchNorm1d(3)))
+    drop = nn.Sequential(nn.Linear(2, 3), nn.Dropout(0.5))
+    assert not _pure_forward(drop)
+    drop.eval()
+    assert _pure_forward(drop)
