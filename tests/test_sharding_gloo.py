@@ -238,3 +238,85 @@ def test_round_driver_shard_over_option():
     assert f.func is ShardedSerialAggregator and "group" not in f.keywords
     with pytest.raises(ValueError):
         make(shard_over="group", aggregator_factory=partial(SerialAggregator))
+
+
+def _api_worker(rank, world, port, outdir):
+    """Every SerialAggregator call on a parameter-sharded key, including
+    shards that are empty (P < 64 * world), against the one-process oracle."""
+    import json
+
+    import torch.distributed as dist
+
+    from fedsim_amd import ops
+    from fedsim_amd.sharding import ShardedSerialAggregator
+    from shard_oracle import OracleEntry
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        for P in (1, 63, 65, 130, 4099):
+            K = 7
+            X = V.client_rows("realistic", K, P, P)
+            w = V.client_weights("fedavg", K, P)
+            w[3] = 0  # a zero weight is added (its product is +0.0)
+            agg = ShardedSerialAggregator(entry_factory=OracleEntry)
+            for k in range(K):
+                agg.add("p", torch.from_numpy(X[k].copy()), w[k])
+                agg.add("clients.train.loss", 0.5 + k, w[k])  # host scalar key
+                if k == 2:
+                    out[f"{P}/get2"] = agg.get("p").numpy().tolist()
+            out[f"{P}/sum"] = agg.get_sum("p").numpy().tolist()
+            out[f"{P}/weight"] = agg.get_weight("p")
+            out[f"{P}/keys"] = sorted(agg.keys())
+            out[f"{P}/shard"] = agg.shard_of("p")
+            cloud = torch.from_numpy(V.cloud_vector(P, 1))
+            buf, grad = torch.empty(P), torch.empty(P)
+            step = ops.ServerStep("fedavg", cloud, lr=0.3, momentum=0.9, momentum_buf=buf,
+                                  momentum_init=True, grad_out=grad)
+            agg.pop_step("p", step)
+            out[f"{P}/cloud"] = cloud.numpy().tolist()
+            out[f"{P}/buf"] = buf.numpy().tolist()
+            rep = agg.pop_all()
+            out[f"{P}/report"] = float(rep["clients.train.loss"])
+            assert "p" not in agg
+        with open(os.path.join(outdir, f"api{rank}.json"), "w") as f:
+            json.dump(out, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_aggregator_api_every_rank():
+    import json
+
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_api_worker, args=(world, _free_port(), d), nprocs=world, join=True,
+                           start_method="spawn")
+        got = [json.load(open(os.path.join(d, f"api{r}.json"))) for r in range(world)]
+    for P in (1, 63, 65, 130, 4099):
+        K = 7
+        X = V.client_rows("realistic", K, P, P)
+        w = V.client_weights("fedavg", K, P)
+        w[3] = 0
+        exp2 = ref.reduce(X[:3], w[:3], W=sum(w[:3]))
+        exps = ref.reduce(X, w)
+        st = ref.ServerState("fedavg", V.cloud_vector(P, 1), dict(lr=0.3, momentum=0.9))
+        st.step(ref.reduce(X, w, W=sum(w)))
+        loss = sum((0.5 + k) * w[k] for k in range(K)) / sum(w)
+        spans = []
+        for r in range(world):
+            g = got[r]
+            np.testing.assert_array_equal(bits(np.array(g[f"{P}/get2"], np.float32)), bits(exp2))
+            np.testing.assert_array_equal(bits(np.array(g[f"{P}/sum"], np.float32)), bits(exps))
+            np.testing.assert_array_equal(bits(np.array(g[f"{P}/cloud"], np.float32)),
+                                          bits(st.cloud))
+            np.testing.assert_array_equal(bits(np.array(g[f"{P}/buf"], np.float32)), bits(st.buf))
+            assert g[f"{P}/weight"] == sum(w)
+            assert g[f"{P}/keys"] == ["clients.train.loss", "p"]
+            assert g[f"{P}/report"] == loss
+            spans.append(tuple(g[f"{P}/shard"]))
+        # the shards tile [0, P): equal 64-aligned widths, empty past the end
+        assert spans[0][0] == 0 and spans[-1][1] == P
+        for (a, b), (c, e) in zip(spans, spans[1:]):
+            assert b == c
