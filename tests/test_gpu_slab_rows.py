@@ -257,3 +257,33 @@ def test_pack_segments_random_layouts(seed):
     others = [k for k in range(Kcap) if k != r]
     if others:
         assert torch.isnan(Xb[:, others, :]).all()
+
+
+def test_slab_rows_carry_special_values_bitwise():
+    """-0.0, subnormals, +-inf, NaN and huge values in the parameters go
+    through the pack unchanged and reduce as the reference's arithmetic does
+    (the oracle on the same vectors)."""
+    from fedsim_amd.utils import vectorize_module
+
+    specials = torch.tensor([-0.0, 0.0, 1e-45, -1e-40, 3e38, -3e38, float("inf"),
+                             float("-inf"), float("nan"), 1.0, -2.5])
+    K = 6
+    models, vecs = [], []
+    for k in range(K):
+        torch.manual_seed(300 + k)
+        m = Odd(30).to(DEV)
+        with torch.no_grad():
+            m.d.view(-1)[: specials.numel()] = specials.roll(k).to(DEV)
+            m.a.weight.view(-1)[k] = -0.0
+        models.append(m)
+        vecs.append(parameters_to_vector(m.parameters()).detach().cpu().numpy())
+    P = vecs[0].size
+    w = [int(v) for v in np.random.default_rng(9).integers(50, 601, size=K)]
+    agg = _agg(borrow=True)
+    for k in range(K):
+        agg.add("p", vectorize_module(models[k], out=agg.reserve("p", P, DEV)), w[k])
+    out = agg.pop("p").cpu().numpy()
+    exp = ref.reduce(np.stack(vecs), w, W=sum(w))
+    nan = np.isnan(exp)
+    assert nan.any() and np.array_equal(np.isnan(out), nan)  # NaN payloads may differ
+    np.testing.assert_array_equal(bits(out[~nan]), bits(exp[~nan]))
