@@ -35,6 +35,7 @@ FEDAGG_FLAT = 0x10000
 FEDAGG_LDSW = 0x20000
 FEDAGG_MAP_SHIFT = 18
 FEDAGG_FAST = 0x200000
+FEDAGG_RELU = 0x400000
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0
@@ -113,6 +114,12 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
          ctypes.c_void_p, ctypes.c_void_p],
+    ),
+    "fedagg_teacher_linear_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
     ),
     "fedagg_finalize_f32": (
         ctypes.c_int,

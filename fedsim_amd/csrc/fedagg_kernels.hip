@@ -1441,6 +1441,104 @@ hipError_t with_step(int algo, bool mom, const StepPtrs& sp, F&& f) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// FedDF teacher ensemble (fedsim/distributed/centralized/training/feddf.py
+// :117-122): one nn.Linear layer of K stacked teacher models on the matrix
+// cores.  y[k, m, n] = act(sum_i x[k, m, i] * W_k[n, i] + b_k[n]) with W_k /
+// b_k read from teacher k's flat parameter vector (a row of the [K, P] slab,
+// parameters_to_vector layout: W row-major [out, in], then b).
+//
+// A workgroup (4 waves) owns a 64-row x 64-column output tile of one
+// teacher; x and W tiles of 32 inputs are staged through LDS (coalesced rows,
+// zero-filled past the edges) and each wave runs 16 x 64 of the tile as four
+// 16x16 accumulators of v_mfma_f32_16x16x4_f32 (exact f32: a k-ordered fmaf
+// chain per output, the bias added last).  Every teacher's weights are read
+// once per 64-row tile: a FedDF batch (64 samples) reads each teacher once.
+// ---------------------------------------------------------------------------
+constexpr int kTL_M = 64;  // output rows (samples) per workgroup
+constexpr int kTL_N = 64;  // output columns (features) per workgroup
+constexpr int kTL_K = 32;  // inputs per LDS stage
+constexpr int kTL_PAD = 1;
+
+__global__ __launch_bounds__(256) void k_teacher_linear(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t M, int64_t in, int64_t out,
+    float* __restrict__ y, int64_t n_tiles, int64_t m_tiles, int relu) {
+  __shared__ float sx[kTL_M][kTL_K + kTL_PAD];
+  __shared__ float sw[kTL_N][kTL_K + kTL_PAD];
+  const int64_t tile = blockIdx.x;
+  const int64_t k = tile / (n_tiles * m_tiles);
+  const int64_t rem = tile - k * n_tiles * m_tiles;
+  const int64_t m0 = (rem / n_tiles) * kTL_M;
+  const int64_t n0 = (rem % n_tiles) * kTL_N;
+  const float* xk = x + k * x_kstride;
+  const float* wk = params + k * params_kstride + w_off;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // 64 x 32 of x and of W per stage: 2048 floats each, 8 per thread; 32
+  // consecutive lanes read one row's 128 contiguous bytes.  The next stage's
+  // loads are issued into registers before this stage's MFMAs, so their
+  // latency hides behind the matrix work.
+  float rx[8], rw[8];
+  auto fetch = [&](int64_t i0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = t + 256 * j;
+      const int r = e / kTL_K;
+      const int64_t i = i0 + e % kTL_K;
+      const int64_t m = m0 + r;
+      const int64_t n = n0 + r;
+      rx[j] = (m < M && i < in) ? xk[m * in + i] : 0.f;
+      rw[j] = (n < out && i < in) ? wk[n * in + i] : 0.f;
+    }
+  };
+  fetch(0);
+  for (int64_t i0 = 0; i0 < in; i0 += kTL_K) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = t + 256 * j;
+      sx[e / kTL_K][e % kTL_K] = rx[j];
+      sw[e / kTL_K][e % kTL_K] = rw[j];
+    }
+    __syncthreads();
+    if (i0 + kTL_K < in) fetch(i0 + kTL_K);
+    const int row = lane & 15;
+    const int kk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < kTL_K / 4; ++s) {
+      // A[row][k] = x[m0 + 16 wave + row][i0 + 4 s + k];  B[k][col] = W[n0 + 16 j + col][...]
+      const float a = sx[wave * 16 + row][4 * s + kk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float b = sw[j * 16 + row][4 * s + kk];
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // C/D: col = lane & 15, row = (lane >> 4) * 4 + reg
+  const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
+  float* yk = y + k * M * out;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = n0 + j * 16 + (lane & 15);
+    if (n >= out) continue;
+    const float bias = bk ? bk[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = m0 + wave * 16 + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+      float v = acc[j][r] + bias;
+      if (relu) v = v > 0.f ? v : 0.f;
+      yk[m * out + n] = v;
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1588,6 +1686,27 @@ int fedagg_unpack_row_f32(const float* Xb, int64_t Kcap, int64_t C, int64_t r, i
   if (!Xb || !dst || !aligned16(Xb) || !aligned16(dst)) return FEDAGG_EINVAL;
   hipLaunchKernelGGL(k_unpack_row, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), Xb, Kcap, C, r, P, dst);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* params,
+                              int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t K,
+                              int64_t M, int64_t in, int64_t out, float* y, int flags,
+                              void* stream) {
+  if (K < 0 || M < 0 || in <= 0 || out <= 0 || x_kstride < 0 || params_kstride < 0 ||
+      w_off < 0 || b_off < -1)
+    return FEDAGG_EINVAL;
+  if (flags & ~FEDAGG_RELU) return FEDAGG_EINVAL;
+  if (K == 0 || M == 0) return 0;
+  if (!x || !params || !y) return FEDAGG_EINVAL;
+  const int64_t n_tiles = (out + kTL_N - 1) / kTL_N;
+  const int64_t m_tiles = (M + kTL_M - 1) / kTL_M;
+  const int64_t tiles = K * n_tiles * m_tiles;
+  if (tiles > (int64_t(1) << 31) - 1) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_teacher_linear, dim3(static_cast<unsigned>(tiles)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), x, x_kstride, params, params_kstride,
+                     w_off, b_off, M, in, out, y, n_tiles, m_tiles,
+                     (flags & FEDAGG_RELU) ? 1 : 0);
   return static_cast<int>(hipGetLastError());
 }
 

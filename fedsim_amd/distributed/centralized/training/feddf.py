@@ -15,8 +15,12 @@ MI355X-first differences (same results):
   are stacked once per round into one [K, P] HBM slab and each teacher runs
   through ``functional_call`` on views of its row.
 * On a HIP device, and for models without buffers, the K teacher forwards run
-  as ONE batched forward (``torch.func.vmap`` over the slab rows, chunked to
-  bound activation memory) into a [K, B*C] logits slab, and the teacher
+  as ONE batched forward into a [K, B*C] logits slab: the model's traced graph
+  replayed over all K teachers, its ``nn.Linear`` layers on the matrix cores
+  (``fedagg_teacher_linear_f32``, v_mfma_f32_16x16x4_f32, ReLU fused;
+  teacher_program.py) and the rest under ``torch.vmap``; a model that does
+  not trace keeps the whole-model ``vmap`` over the slab rows (chunked to
+  bound activation memory).  The teacher
   average is one launch of the exact-mode reduce kernel
   (``fedagg_reduce_f32``, weights 1, divide by fl32(K)): the same per-element
   arithmetic and order as the reference's ``add(target, 1)`` x K + ``get``.
@@ -43,6 +47,7 @@ from torch.nn.functional import log_softmax
 from .... import ops
 from ....scores import KLDivScore
 from ....utils import SerialAggregator, initialize_module, vector_to_named_parameters_like
+from . import teacher_program
 from .fedavg import FedAvg
 from .utils import serial_aggregation
 
@@ -73,7 +78,7 @@ class TeacherEnsemble(object):
     """K teacher parameter vectors stacked in one slab; ``mean_logits(x)`` is
     the reference's weight-1 SerialAggregator average of their outputs."""
 
-    def __init__(self, model, teacher_vectors, device):
+    def __init__(self, model, teacher_vectors, device, program=True):
         self.model = model
         self.named = list(model.named_parameters())
         self.slab = torch.stack([t.reshape(-1) for t in teacher_vectors]).to(device)
@@ -81,9 +86,43 @@ class TeacherEnsemble(object):
         self.batched = (self.slab.device.type == "cuda"
                         and len(list(model.buffers())) == 0)
         self._w32 = None
+        # the traced forward with the Linear layers on the matrix cores
+        # (teacher_program.py); checked against the vmap path on first use
+        self.program = teacher_program.build(model, self.named, self.slab) \
+            if (program and self.batched) else None
+        self._checked = False
 
     def _forward(self, flat, x):
         return functional_call(self.model, vector_to_named_parameters_like(flat, self.named), (x,))
+
+    def _vmap_logits(self, x):
+        chunks = []
+        for k0 in range(0, self.K, _TEACHER_CHUNK):
+            part = self.slab[k0:k0 + _TEACHER_CHUNK]
+            chunks.append(torch.vmap(self._forward, in_dims=(0, None))(part, x))
+        return torch.cat(chunks) if len(chunks) > 1 else chunks[0]
+
+    def teacher_logits(self, x):
+        """[K, ...] outputs of every teacher on ``x`` (batched path)."""
+        if self.program is None:
+            return self._vmap_logits(x)
+        if self._checked:
+            return self.program(x)
+        # first use: the program must reproduce the vmap'd forward (same
+        # graph, f32 matrix-core arithmetic: normwise), else it is dropped
+        ref = self._vmap_logits(x)
+        try:
+            got = self.program(x)
+            ok = (got.shape == ref.shape and bool(torch.isfinite(got).all() == torch.isfinite(ref).all())
+                  and float(torch.linalg.vector_norm((got - ref).double().nan_to_num())) <=
+                  1e-4 * float(torch.linalg.vector_norm(ref.double().nan_to_num())) + 1e-30)
+        except Exception:  # noqa: BLE001 - a graph the replay cannot run: keep vmap
+            got, ok = None, False
+        self._checked = True
+        if not ok:
+            self.program = None
+            return ref
+        return got
 
     @torch.no_grad()
     def mean_logits(self, x):
@@ -92,11 +131,7 @@ class TeacherEnsemble(object):
             for k in range(self.K):
                 agg.add("target", self._forward(self.slab[k], x).clone(), 1)
             return agg.get("target")
-        chunks = []
-        for k0 in range(0, self.K, _TEACHER_CHUNK):
-            part = self.slab[k0:k0 + _TEACHER_CHUNK]
-            chunks.append(torch.vmap(self._forward, in_dims=(0, None))(part, x))
-        logits = torch.cat(chunks) if len(chunks) > 1 else chunks[0]
+        logits = self.teacher_logits(x)
         K, shape = logits.shape[0], logits.shape[1:]
         rows = logits.reshape(K, -1).float().contiguous()
         if self._w32 is None:

@@ -378,6 +378,33 @@ def unpack_row(Xb: torch.Tensor, r: int, P: int, out: Optional[torch.Tensor] = N
     return out
 
 
+def teacher_linear(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int, in_f: int,
+                   out_f: int, shared: bool, relu: bool = False) -> torch.Tensor:
+    """One nn.Linear layer of the K teacher models whose flat parameter
+    vectors are the rows of ``slab`` ([K, P], parameters_to_vector layout),
+    on the matrix cores (fedagg_teacher_linear_f32).  ``x``: [M, in] shared by
+    every teacher (``shared``) or [K, M, in].  Returns y [K, M, out]
+    (ReLU applied when ``relu``).  b_off = -1: no bias."""
+    _require_hip_f32(x, "x")
+    _require_hip_f32(slab, "slab")
+    if slab.dim() != 2 or not slab.is_contiguous() or x.device != slab.device:
+        raise ValueError("slab must be a contiguous [K, P] tensor on x's device")
+    if not x.is_contiguous() or x.shape[-1] != in_f:
+        raise ValueError(f"x must be contiguous with a last dimension of {in_f}")
+    K, P = slab.shape
+    if w_off < 0 or w_off + in_f * out_f > P or (b_off >= 0 and b_off + out_f > P):
+        raise ValueError("layer offsets outside the parameter vector")
+    M = x.numel() // in_f if shared else x.numel() // (in_f * max(K, 1))
+    if not shared and x.shape[0] != K:
+        raise ValueError("a per-teacher x must have K rows in its first dimension")
+    y = torch.empty((K, M, out_f), dtype=torch.float32, device=x.device)
+    rc = _native.load().fedagg_teacher_linear_f32(
+        x.data_ptr(), 0 if shared else M * in_f, slab.data_ptr(), P, w_off, b_off, K, M, in_f,
+        out_f, y.data_ptr(), _native.FEDAGG_RELU if relu else 0, _stream_ptr(x.device))
+    check(rc, "fedagg_teacher_linear_f32")
+    return y
+
+
 def finalize(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = fl32(acc / fl32(W)) — SerialAggregator.pop's true division."""
     _require_hip_f32(acc, "acc")

@@ -100,6 +100,9 @@ extern "C" {
  * gamma_K forward-error bound), not bitwise.  Ignored (exact kernels) where it
  * would not add parallelism. */
 #define FEDAGG_FAST     0x200000
+/* fedagg_teacher_linear_f32: apply ReLU to the layer's output (a following
+ * torch.relu / nn.ReLU fused into the layer) */
+#define FEDAGG_RELU     0x400000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
@@ -165,6 +168,24 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B,
 int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,
                               int64_t B, int64_t P, const float* acc_in, float* out,
                               float W32, int flags, void* stream);
+
+/*
+ * FedDF's teacher ensemble (fedsim/distributed/centralized/training/feddf.py
+ * :117-122 runs every client model on each distillation batch): ONE nn.Linear
+ * layer of K stacked teacher models, on the matrix cores (f32 in / f32
+ * accumulate):
+ *   y[k][m][n] = act(sum_i x[k*x_kstride + m*in + i] * W_k[n][i] + b_k[n])
+ * W_k = params + k*params_kstride + w_off ([out, in] row-major, the teacher's
+ * flat vector in parameters_to_vector order); b_k = params + k*params_kstride
+ * + b_off (b_off = -1: no bias).  x_kstride = 0 shares one input across the
+ * teachers (the batch itself).  y is [K, M, out] contiguous.  flags:
+ * FEDAGG_RELU.  Results are exact f32 k-ordered fmaf chains (the bias added
+ * last): normwise, not bitwise, equal to a CPU / BLAS Linear.
+ */
+int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* params,
+                              int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t K,
+                              int64_t M, int64_t in, int64_t out, float* y, int flags,
+                              void* stream);
 
 /*
  * vectorize_module straight into a slab row (fedsim/utils/convert_parameters.py

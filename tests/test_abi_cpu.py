@@ -43,7 +43,8 @@ def test_header_declares_the_abi():
         "fedagg_abi_version", "fedagg_strerror", "fedagg_column_mapping", "fedagg_reduce_f32",
         "fedagg_reduce_rows_f32",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_pack_segments_f32",
-        "fedagg_unpack_row_f32", "fedagg_finalize_f32", "fedagg_fedavg_sgd_f32",
+        "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_finalize_f32",
+        "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
         "fedagg_reduce_step_blocked_f32", "fedagg_reduce_step_rows_f32",
     ])

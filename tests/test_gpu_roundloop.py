@@ -104,7 +104,9 @@ def test_round_loop_matches_reference(run, device, arrays):
 
 
 def test_feddf_teacher_average_is_the_exact_kernel_mean():
-    """FedDF's batched teacher path: K teacher forwards in one vmap'd forward,
+    """FedDF's batched teacher path: K teacher forwards in one batched
+    forward (the traced replay with its Linear layers on the matrix cores,
+    teacher_program.py; the vmap'd forward for models it cannot replay),
     averaged by fedagg_reduce_f32 — bitwise the reference's weight-1
     SerialAggregator mean (aggregators.py:23-60) of the SAME logits, and
     within fp32 rounding of the one-teacher-at-a-time forwards."""
@@ -122,8 +124,8 @@ def test_feddf_teacher_average_is_the_exact_kernel_mean():
     x = torch.randn(33, 37, device=dev)
     got = ens.mean_logits(x)
     per = torch.stack([ens._forward(t, x) for t in teachers])  # [K, B, C]
-    batched = torch.cat([torch.vmap(ens._forward, in_dims=(0, None))(ens.slab[k:k + 64], x)
-                         for k in range(0, 70, 64)])
+    assert ens.program is not None  # TinyModel replays: both Linear layers on MFMA
+    batched = ens.program(x)
     want = ref.reduce(batched.reshape(70, -1).cpu().numpy(), [1] * 70, W=70)
     np.testing.assert_array_equal(bits(got.reshape(-1).cpu().numpy()), bits(want))
     torch.testing.assert_close(got, per.mean(0), rtol=1e-5, atol=1e-6)

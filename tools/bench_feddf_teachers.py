@@ -1,0 +1,107 @@
+"""FedDF's teacher forwards per distillation batch: the traced replay with
+the Linear layers on the matrix cores (teacher_program.py) against the
+whole-model torch.vmap over the teacher slab, for the reference's model
+shapes (SimpleMLP 784-200-200-10 on MNIST, SimpleCNN2 on CIFAR-100), B = 64
+(the server's test_batch_size), K teachers.  Kernel time from HIP events,
+median of repeated calls.
+
+python tools/bench_feddf_teachers.py [--K 10,100,1000]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+from torch import nn
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fedsim_amd.distributed.centralized.training.feddf import TeacherEnsemble  # noqa: E402
+
+
+class SimpleMLP(nn.Module):  # fedsim/models/simple_models.py:23 (Resize is the identity at 28x28)
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(784, 200)
+        self.fc2 = nn.Linear(200, 200)
+        self.classifier = nn.Linear(200, 10)
+
+    def forward(self, x):
+        x = torch.flatten(x, 1)
+        x = torch.relu(self.fc1(x))
+        x = torch.relu(self.fc2(x))
+        return self.classifier(x)
+
+
+class SimpleCNN2(nn.Module):  # fedsim/models/simple_models.py:165-255, num_classes=100
+    """The reference's forward after its Resize to 24 x 24 (inputs are fed at
+    24 x 24 here; torchvision is not installed)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 5, padding="same")
+        self.conv2 = nn.Conv2d(64, 64, 5, padding="same")
+        self.fc1 = nn.Linear(64 * 6 * 6, 384)
+        self.fc2 = nn.Linear(384, 192)
+        self.classifier = nn.Linear(192, 100)
+
+    def forward(self, x):
+        F = torch.nn.functional
+        x = F.relu(self.conv1(x))
+        x = F.pad(x, (0, 1, 0, 1), value=0)
+        x = F.local_response_norm(x, size=4, alpha=0.001 / 9)
+        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=0)
+        x = F.relu(self.conv2(x))
+        x = F.local_response_norm(x, size=4, alpha=0.001 / 9)
+        x = F.pad(x, (0, 1, 0, 1), value=0)
+        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=0)
+        x = x.view(x.shape[0], -1)
+        x = F.relu(self.fc1(x))
+        x = F.relu(self.fc2(x))
+        return self.classifier(x)
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    return float(np.median(ms))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", default="10,100,1000")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for name, cls, shape in (("SimpleMLP", SimpleMLP, (64, 1, 28, 28)),
+                             ("SimpleCNN2", SimpleCNN2, (64, 3, 24, 24))):
+        torch.manual_seed(0)
+        model = cls().to(dev)
+        P = sum(p.numel() for p in model.parameters())
+        x = torch.randn(*shape, device=dev)
+        for K in [int(v) for v in a.K.split(",")]:
+            base = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+            teachers = [base + 0.05 * torch.randn_like(base) for _ in range(K)]
+            ens = TeacherEnsemble(model, teachers, dev)
+            ens.mean_logits(x)  # first-batch check
+            kept = ens.program is not None
+            t_prog = timed(lambda: ens.mean_logits(x)) if kept else None
+            vm = TeacherEnsemble(model, teachers, dev, program=False)
+            t_vmap = timed(lambda: vm.mean_logits(x))
+            print(json.dumps(dict(model=name, P=P, K=K, B=shape[0], program_kept=kept,
+                                  matrix_core_ms=t_prog, vmap_ms=t_vmap,
+                                  speedup=(t_vmap / t_prog) if t_prog else None)), flush=True)
+            del ens, vm, teachers
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
