@@ -1697,6 +1697,9 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
       w_off < 0 || b_off < -1)
     return FEDAGG_EINVAL;
   if (flags & ~FEDAGG_RELU) return FEDAGG_EINVAL;
+  // with several teachers, the layer must lie inside one teacher's vector
+  if (K > 1 && (w_off + in * out > params_kstride || (b_off >= 0 && b_off + out > params_kstride)))
+    return FEDAGG_EINVAL;
   if (K == 0 || M == 0) return 0;
   if (!x || !params || !y) return FEDAGG_EINVAL;
   const int64_t n_tiles = (out + kTL_N - 1) / kTL_N;
