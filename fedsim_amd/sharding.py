@@ -130,6 +130,9 @@ def client_sharded_chain(X_local: torch.Tensor, w32_local: torch.Tensor, W,
     running sum of ranks 0..r-1 for that block.  The final (finalized) result
     is produced on the last rank and broadcast to all ranks in ``out``.
     """
+    if X_local.dim() != 2:
+        raise ValueError("client_sharded_chain takes row-major [K_local, P] client rows "
+                         "(its column blocks are column slices of them)")
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     P = out.numel()
