@@ -187,3 +187,81 @@ def test_mapping_random(dev, r, mapping, unroll, layout, split):
     else:
         call(0, K, None, True)
     same(out.cpu().numpy(), ref.reduce(X, w, W=W))
+
+
+class _TwoParams(torch.nn.Module):
+    """A client model whose flat vector is one client row (two ragged
+    parameter tensors, so the pack walks a segment boundary)."""
+
+    def __init__(self, P, dev):
+        super().__init__()
+        a = max(1, P // 3)
+        self.a = torch.nn.Parameter(torch.empty(a, device=dev))
+        self.b = torch.nn.Parameter(torch.empty(P - a, device=dev)) if P > a else None
+
+    def load(self, row):
+        with torch.no_grad():
+            self.a.copy_(row[: self.a.numel()])
+            if self.b is not None:
+                self.b.copy_(row[self.a.numel():])
+
+
+@SETTINGS
+@given(rounds(max_k=20, max_p=4000), st.integers(1, 7), st.booleans(),
+       st.lists(st.integers(0, 4), min_size=20, max_size=20),
+       st.sampled_from(["pop", "fedavg", "adabest"]))
+def test_mixed_sources_random_stream(dev, r, max_rows, borrow, kinds, final):
+    """Every way a client vector reaches the aggregator, interleaved at
+    random in one round: pageable host, pinned host (overwritten right after
+    add), HBM (borrowed or packed), a model vectorized into a reserved slab
+    row, and a reservation whose client never arrives; a mid-stream get; then
+    pop or the fused pop + server step.  Bitwise vs the oracle."""
+    from fedsim_amd import ops
+    from fedsim_amd.utils import SerialAggregator, vectorize_module
+
+    X, w = r
+    K, P = X.shape
+    agg = SerialAggregator(max_rows=max_rows, borrow=borrow)
+    model = _TwoParams(P, dev)
+    pinned = torch.empty(P).pin_memory()
+    for k in range(K):
+        kind = kinds[k]
+        if kind == 4:
+            agg.reserve("p", P, dev)  # a client that diverges after its reservation
+            kind = k % 4
+        if kind == 0:
+            src = torch.from_numpy(X[k].copy())
+        elif kind == 1:
+            pinned.copy_(torch.from_numpy(X[k]))
+            src = pinned
+        elif kind == 2:
+            src = torch.from_numpy(X[k].copy()).to(dev)
+        else:
+            model.load(torch.from_numpy(X[k]).to(dev))
+            src = vectorize_module(model, out=agg.reserve("p", P, dev))
+        agg.add("p", src, w[k])
+        if kind == 1:
+            pinned.fill_(float("nan"))
+        if k == K // 2:
+            W2 = sum(w[: k + 1])
+            same(agg.get("p").cpu().numpy(), ref.reduce(X[: k + 1], w[: k + 1], W=W2 or None))
+    if K == 0:
+        assert "p" not in agg
+        return
+    W = sum(w)
+    avg = ref.reduce(X, w, W=W if W else None)
+    if final == "pop":
+        same(agg.pop("p").cpu().numpy(), avg)
+        return
+    cloud0 = np.random.default_rng(K * 7 + P).normal(0, 0.05, P).astype(np.float32)
+    aux0 = np.random.default_rng(P).normal(0, 0.05, P).astype(np.float32)
+    st_ = ref.ServerState(final, cloud0, dict(lr=0.3, momentum=0.9),
+                          aux=aux0 if final == "adabest" else None, coef=0.6)
+    st_.step(avg)
+    cloud = torch.from_numpy(cloud0.copy()).to(dev)
+    aux = torch.from_numpy(aux0.copy()).to(dev) if final == "adabest" else None
+    buf = torch.empty_like(cloud)
+    agg.pop_step("p", ops.ServerStep(final, cloud, lr=0.3, momentum=0.9, coef=0.6, aux=aux,
+                                     momentum_buf=buf, momentum_init=True))
+    same(cloud.cpu().numpy(), st_.cloud)
+    same(buf.cpu().numpy(), st_.buf)
