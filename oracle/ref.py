@@ -45,8 +45,11 @@ def lib():
         L.ref_feddyn_sgd_f32.argtypes = [vp, f32, f32, vp, vp, vp, vp, i64]
         L.ref_server_step_f32.argtypes = [ci, vp, f32, vp, vp, vp, vp, ci, vp, f32, f32, f32,
                                           f32, ci, ci, i64]
+        L.ref_teacher_linear_f32.argtypes = [vp, i64, vp, i64, i64, i64, i64, i64, i64, i64,
+                                             vp, ci]
         for fn in ("ref_reduce_f32", "ref_finalize_f32", "ref_fedavg_sgd_f32",
-                   "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32", "ref_server_step_f32"):
+                   "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32", "ref_server_step_f32",
+                   "ref_teacher_linear_f32"):
             getattr(L, fn).restype = None
         _lib = L
     return _lib
@@ -172,3 +175,17 @@ def reduce_numpy(X: np.ndarray, weights: Sequence) -> np.ndarray:
 
 def finalize_numpy(acc: np.ndarray, W) -> np.ndarray:
     return (acc / np.float32(W)).astype(np.float32)
+
+
+def teacher_linear(x: np.ndarray, slab: np.ndarray, w_off: int, b_off: int, in_f: int,
+                   out_f: int, shared: bool, relu: bool = False) -> np.ndarray:
+    """C oracle of fedagg_teacher_linear_f32 (an f32 fmaf chain in input
+    order; see fedagg_ref.c)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    slab = np.ascontiguousarray(slab, dtype=np.float32)
+    K, P = slab.shape
+    M = x.size // in_f if shared else x.size // (in_f * K)
+    y = np.empty((K, M, out_f), dtype=np.float32)
+    lib().ref_teacher_linear_f32(_p(x), 0 if shared else M * in_f, _p(slab), P, w_off, b_off,
+                                 K, M, in_f, out_f, _p(y), int(relu))
+    return y

@@ -91,3 +91,27 @@ def test_ensemble_keeps_the_matrix_core_path():
     logits = ens.program(x).reshape(33, -1).cpu().numpy()
     exp = ref.reduce(logits, [1] * 33, W=33)
     np.testing.assert_array_equal(bits(mean.reshape(-1).cpu().numpy()), bits(exp))
+
+
+@pytest.mark.parametrize("M,in_f,out_f", [(1, 1, 1), (63, 3, 65), (64, 37, 11), (65, 784, 200),
+                                          (130, 200, 10), (7, 33, 129)])
+@pytest.mark.parametrize("shared", [True, False])
+def test_teacher_linear_kernel_is_the_fmaf_chain(M, in_f, out_f, shared):
+    """Bitwise against the C oracle's restatement (oracle/fedagg_ref.c
+    ref_teacher_linear_f32): each output is an f32 fmaf chain over the inputs
+    in order, then one bias add -- what v_mfma_f32_16x16x4_f32 computes."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    g = torch.Generator(device=DEV).manual_seed(M + 17 * in_f + out_f)
+    K = 3
+    P = 5 + in_f * out_f + out_f
+    slab = torch.randn(K, P, device=DEV, generator=g)
+    x = torch.randn((M, in_f) if shared else (K, M, in_f), device=DEV, generator=g)
+    for relu in (False, True):
+        y = ops.teacher_linear(x, slab, 5, 5 + in_f * out_f, in_f, out_f, shared=shared,
+                               relu=relu)
+        exp = ref.teacher_linear(x.cpu().numpy(), slab.cpu().numpy(), 5, 5 + in_f * out_f, in_f,
+                                 out_f, shared, relu)
+        np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp))
