@@ -245,11 +245,29 @@ class _ShardEntry(_TensorEntry):
 
     def pop_step(self, step: ops.ServerStep) -> None:
         """This rank's shard of pop + server step (ServerStep.narrow), then
-        every operand the step wrote is re-assembled on every rank."""
+        every operand the step wrote is re-assembled on every rank, all of
+        them in ONE all-gather (a [n_operands, S] block per rank)."""
         if self.inner is not None:
             self.inner.pop_step(step.narrow(self.lo, self.hi))
-        for t in step.outputs():
-            self._gather_into(t, None)
+        outs = step.outputs()
+        if self.agg._world == 1:
+            return
+        if len(outs) == 1:
+            self._gather_into(outs[0], None)
+            return
+        full0 = outs[0]
+        via_host = full0.device.type == "cuda" and \
+            dist.get_backend(self.agg._group) == dist.Backend.GLOO
+        n, S, width = len(outs), self.S, self.hi - self.lo
+        mine = torch.zeros((n, S), dtype=full0.dtype, device="cpu" if via_host else full0.device)
+        for j, t in enumerate(outs):
+            mine[j, :width].copy_(t[self.lo:self.hi])
+        ws = mine.new_empty((self.agg._world, n, S))
+        dist.all_gather_into_tensor(ws.view(-1), mine.view(-1), group=self.agg._group)
+        for j, t in enumerate(outs):
+            # rank r's shard of operand j is ws[r, j, :]: the ranks' shards
+            # are consecutive S-column spans of [0, P)
+            t.copy_(ws[:, j, :].reshape(-1)[: self.P])
 
 
 class _DevicesEntry(_TensorEntry):
