@@ -115,3 +115,32 @@ def test_teacher_linear_kernel_is_the_fmaf_chain(M, in_f, out_f, shared):
         exp = ref.teacher_linear(x.cpu().numpy(), slab.cpu().numpy(), 5, 5 + in_f * out_f, in_f,
                                  out_f, shared, relu)
         np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp))
+
+
+def test_teacher_linear_random_shapes_bitwise():
+    """Random layer shapes, offsets and teacher counts (seeded), bitwise vs
+    the C oracle's fmaf chain, including special values in the inputs."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    rng = np.random.default_rng(2026)
+    for _ in range(40):
+        K = int(rng.integers(1, 6))
+        M = int(rng.integers(1, 150))
+        in_f = int(rng.integers(1, 300))
+        out_f = int(rng.integers(1, 150))
+        w_off = int(rng.integers(0, 9))
+        bias = bool(rng.integers(0, 2))
+        P = w_off + in_f * out_f + (out_f if bias else 0) + int(rng.integers(0, 5))
+        slab = rng.standard_normal((K, P)).astype(np.float32)
+        shared = bool(rng.integers(0, 2))
+        x = rng.standard_normal((M, in_f) if shared else (K, M, in_f)).astype(np.float32)
+        x.reshape(-1)[:: max(1, x.size // 7)] = np.float32(-0.0)
+        relu = bool(rng.integers(0, 2))
+        b_off = w_off + in_f * out_f if bias else -1
+        y = ops.teacher_linear(torch.from_numpy(x).to(DEV), torch.from_numpy(slab).to(DEV),
+                               w_off, b_off, in_f, out_f, shared=shared, relu=relu)
+        exp = ref.teacher_linear(x, slab, w_off, b_off, in_f, out_f, shared, relu)
+        np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp),
+                                      err_msg=f"K={K} M={M} in={in_f} out={out_f}")
