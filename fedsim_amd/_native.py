@@ -73,6 +73,25 @@ class StepArgs(ctypes.Structure):
     ]
 
 
+class Conv2dShape(ctypes.Structure):
+    """struct fedagg_conv2d_shape (include/fedagg.h)."""
+
+    _fields_ = [(n, ctypes.c_int64) for n in
+                ("M", "C", "H", "W", "OC", "KH", "KW", "stride_h", "stride_w", "pad_h", "pad_w",
+                 "OH", "OW")]
+
+
+class PoolArgs(ctypes.Structure):
+    """struct fedagg_pool_args (include/fedagg.h)."""
+
+    _fields_ = ([(n, ctypes.c_int64) for n in
+                 ("N", "C", "H", "W", "pad_top", "pad_bottom", "pad_left", "pad_right",
+                  "lrn_size")]
+                + [(n, ctypes.c_float) for n in ("lrn_alpha", "lrn_beta", "lrn_k")]
+                + [(n, ctypes.c_int64) for n in
+                   ("pool_kh", "pool_kw", "pool_sh", "pool_sw", "pool_ph", "pool_pw")])
+
+
 # (name, restype, argtypes) for every symbol include/fedagg.h declares.
 SIGNATURES = {
     "fedagg_abi_version": (ctypes.c_int, []),
@@ -120,6 +139,22 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
          ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
+    ),
+    "fedagg_teacher_conv2d_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(Conv2dShape), ctypes.c_void_p,
+         ctypes.c_int, ctypes.c_void_p],
+    ),
+    "fedagg_conv_stage": (ctypes.c_int, [ctypes.c_int64]),
+    "fedagg_pool_output": (
+        ctypes.c_int,
+        [ctypes.POINTER(PoolArgs), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+         ctypes.POINTER(ctypes.c_int64)],
+    ),
+    "fedagg_pad_lrn_maxpool_f32": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(PoolArgs), ctypes.c_void_p, ctypes.c_void_p],
     ),
     "fedagg_finalize_f32": (
         ctypes.c_int,

@@ -97,6 +97,7 @@ constexpr int64_t kNarrowShortB = 64;
 // nontemporal builtin).
 using f32x4 = float __attribute__((ext_vector_type(4)));
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+using f32x16 = float __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------------------
 // Row addressing policies
@@ -1539,6 +1540,232 @@ __global__ __launch_bounds__(256) void k_teacher_linear(
   }
 }
 
+// ---------------------------------------------------------------------------
+// FedDF teacher ensemble, convolutional layers: one nn.Conv2d (groups 1,
+// dilation 1, zero padding) of K stacked teachers as an implicit GEMM on the
+// matrix cores.  Per teacher k the GEMM is
+//     Y[oc][p] = sum_r W_k[oc][r] * X_k[r][p]      r = (c, kh, kw), p = (m, oh, ow)
+// W_k is the conv weight exactly as it lies in the teacher's flat vector
+// ([OC, C, KH, KW] row-major = [OC][R]); X_k is the im2col of the input,
+// never materialised: each stage gathers RK reductions x 256 pixels of it
+// from the input (L1/L2-resident: a 5x5 window reads each input element 25
+// times) straight into LDS.  A workgroup (4 waves) owns 64 output channels x
+// 256 pixels; a wave owns 64 x 64 as 2 x 2 tiles of v_mfma_f32_32x32x2_f32
+// (one A and one B VGPR per 4096 flop, so LDS traffic stays far below the
+// matrix rate).  The next stage's global loads are issued into registers
+// before this stage's MFMAs.  Exact f32: each output is the r-ordered fmaf
+// chain (zero-filled tail to a multiple of RK), then the bias, then ReLU.
+// ---------------------------------------------------------------------------
+constexpr int kTC_OC = 64;    // output channels per workgroup
+constexpr int kTC_PX = 256;   // output pixels per workgroup (64 per wave)
+constexpr int kTC_WPAD = 1;   // sW row pad: 32 lanes reading 32 rows hit 32 banks
+constexpr int kTC_XPAD = 32;  // sX row pad: rows r and r+1 land on different bank halves
+
+template <int RK>
+__global__ __launch_bounds__(256) void k_teacher_conv2d(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s,
+    float* __restrict__ y, int64_t oc_tiles, int64_t px_tiles, int relu) {
+  __shared__ float sW[kTC_OC][RK + kTC_WPAD];
+  __shared__ float sX[RK][kTC_PX + kTC_XPAD];
+  const int64_t tile = blockIdx.x;
+  const int64_t k = tile / (oc_tiles * px_tiles);
+  const int64_t rem = tile - k * oc_tiles * px_tiles;
+  const int64_t oc0 = (rem / px_tiles) * kTC_OC;
+  const int64_t px0 = (rem % px_tiles) * kTC_PX;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int64_t OHW = s.OH * s.OW;
+  const int64_t NPX = s.M * OHW;
+  const int64_t HW = s.H * s.W;
+  const int64_t R = s.C * s.KH * s.KW;
+  const float* wk = params + k * params_kstride + w_off;
+  // this thread gathers pixel px0 + t of the tile
+  const int64_t px = px0 + t;
+  const bool px_ok = px < NPX;
+  int ih0 = 0, iw0 = 0;
+  const float* xp = x;
+  if (px_ok) {
+    const int64_t m = px / OHW;
+    const int64_t ohw = px - m * OHW;
+    const int oh = static_cast<int>(ohw / s.OW);
+    const int ow = static_cast<int>(ohw - int64_t(oh) * s.OW);
+    ih0 = oh * static_cast<int>(s.stride_h) - static_cast<int>(s.pad_h);
+    iw0 = ow * static_cast<int>(s.stride_w) - static_cast<int>(s.pad_w);
+    xp = x + k * x_kstride + m * s.C * HW;
+  }
+  const int H = static_cast<int>(s.H), W = static_cast<int>(s.W);
+  const int KH = static_cast<int>(s.KH), KW = static_cast<int>(s.KW);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  constexpr int WPT = kTC_OC * RK / 256;  // weight elements per thread per stage
+  float rw[WPT], rx[RK];
+  // wave-uniform walk of r = (c, kh, kw) through the stage
+  auto fetch = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int e = t + 256 * j;
+      const int64_t oc = oc0 + e / RK;
+      const int64_t r = r0 + e % RK;
+      rw[j] = (oc < s.OC && r < R) ? wk[oc * R + r] : 0.f;
+    }
+    int64_t c = r0 / (s.KH * s.KW);
+    int rr = static_cast<int>(r0 - c * s.KH * s.KW);
+    int kh = rr / KW;
+    int kw = rr - kh * KW;
+#pragma unroll
+    for (int i = 0; i < RK; ++i) {
+      const int ih = ih0 + kh, iw = iw0 + kw;
+      const bool ok = px_ok && (r0 + i < R) && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      rx[i] = ok ? xp[c * HW + ih * W + iw] : 0.f;
+      if (++kw == KW) {
+        kw = 0;
+        if (++kh == KH) {
+          kh = 0;
+          ++c;
+        }
+      }
+    }
+  };
+  fetch(0);
+  for (int64_t r0 = 0; r0 < R; r0 += RK) {
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int e = t + 256 * j;
+      sW[e / RK][e % RK] = rw[j];
+    }
+#pragma unroll
+    for (int i = 0; i < RK; ++i) sX[i][t] = rx[i];
+    __syncthreads();
+    if (r0 + RK < R) fetch(r0 + RK);
+    const int col = lane & 31;
+    const int kk = lane >> 5;
+#pragma unroll
+    for (int st = 0; st < RK / 2; ++st) {
+      // A[i][k] = W[oc0 + 32 a + i][r0 + 2 st + k];  B[k][j] = X[r0 + 2 st + k][64 wave + 32 b + j]
+      const float a0 = sW[col][2 * st + kk];
+      const float a1 = sW[32 + col][2 * st + kk];
+      const float b0 = sX[2 * st + kk][wave * 64 + col];
+      const float b1 = sX[2 * st + kk][wave * 64 + 32 + col];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C/D of 32x32: col = lane & 31 (pixel), row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5) (channel)
+  const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int64_t p = px0 + wave * 64 + b * 32 + (lane & 31);
+    if (p >= NPX) continue;
+    const int64_t m = p / OHW;
+    float* yp = y + (k * s.M + m) * s.OC * OHW + (p - m * OHW);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (oc >= s.OC) continue;
+        float v = acc[a][b][e] + (bk ? bk[oc] : 0.f);
+        if (relu) v = v > 0.f ? v : 0.f;
+        yp[oc * OHW] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The memory-bound chain that follows a convolution in the reference's CNNs
+// (fedsim/models/simple_models.py:245-252, SimpleCNN2: relu -> F.pad(0,1,0,1)
+// -> F.local_response_norm(size 4) -> F.max_pool2d(3, 2); SimpleCNN: relu ->
+// max_pool2d(2, 2, padding 1)) as ONE pass: zero pad, LRN across channels,
+// max pool.  A workgroup owns one image n and a block of CB channels: it
+// builds the padded, normalised planes in LDS (each input element's LRN
+// computed once, its channel window read from L1/L2) and max-pools them from
+// there, so the conv output is read from HBM once and only the pooled output
+// is written.  LRN follows torch.nn.functional.local_response_norm's ATen
+// sequence: s = sum over the window of fl32(x*x) in channel order from +0,
+// avg = s / size, d = pow(fl32(fl32(avg * alpha) + k), beta), y = x / d.
+// Max pool: -inf start, NaN sticks (max_pool2d's CUDA kernel).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict__ x,
+                                                         fedagg_pool_args a, int64_t CB,
+                                                         int64_t OH, int64_t OW,
+                                                         float* __restrict__ y) {
+  extern __shared__ float plane[];
+  const int64_t nblk = (a.C + CB - 1) / CB;
+  const int64_t n = blockIdx.x / nblk;
+  const int64_t c0 = (blockIdx.x - n * nblk) * CB;
+  const int cbn = static_cast<int>(a.C - c0 < CB ? a.C - c0 : CB);
+  const int H = static_cast<int>(a.H), W = static_cast<int>(a.W);
+  const int Hp = H + static_cast<int>(a.pad_top + a.pad_bottom);
+  const int Wp = W + static_cast<int>(a.pad_left + a.pad_right);
+  const int HpWp = Hp * Wp;
+  const int HW = H * W;
+  const int C = static_cast<int>(a.C);
+  const float* xn = x + n * a.C * HW;
+  const int lo = static_cast<int>(a.lrn_size / 2);
+  const float size_f = static_cast<float>(a.lrn_size);
+  for (int q = threadIdx.x; q < HpWp; q += 256) {
+    const int ph = q / Wp;
+    const int ih = ph - static_cast<int>(a.pad_top);
+    const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
+    const bool in = static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                    static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+    const int off = ih * W + iw;
+    for (int cc = 0; cc < cbn; ++cc) {
+      float v = 0.f;
+      if (in) {
+        const int c = static_cast<int>(c0) + cc;
+        v = xn[c * HW + off];
+        if (a.lrn_size > 0) {
+          float sum = 0.f;
+          for (int t = 0; t < a.lrn_size; ++t) {
+            const int ch = c - lo + t;
+            const float u = static_cast<unsigned>(ch) < static_cast<unsigned>(C) ? xn[ch * HW + off] : 0.f;
+            sum = sum + u * u;
+          }
+          const float avg = sum / size_f;
+          const float d = powf(avg * a.lrn_alpha + a.lrn_k, a.lrn_beta);
+          v = v / d;
+        }
+      }
+      plane[cc * HpWp + q] = v;
+    }
+  }
+  __syncthreads();
+  const int OHW = static_cast<int>(OH * OW);
+  const int kh = static_cast<int>(a.pool_kh), kw = static_cast<int>(a.pool_kw);
+  float* yn = y + (n * a.C + c0) * OHW;
+  for (int q = threadIdx.x; q < OHW; q += 256) {
+    const int oh = q / static_cast<int>(OW);
+    const int ow = q - oh * static_cast<int>(OW);
+    const int hs = oh * static_cast<int>(a.pool_sh) - static_cast<int>(a.pool_ph);
+    const int ws = ow * static_cast<int>(a.pool_sw) - static_cast<int>(a.pool_pw);
+    const int he = min(hs + kh, Hp), we = min(ws + kw, Wp);
+    const int h0 = max(hs, 0), w0 = max(ws, 0);
+    for (int cc = 0; cc < cbn; ++cc) {
+      const float* pl = plane + cc * HpWp;
+      float m = -__builtin_inff();
+      for (int h = h0; h < he; ++h)
+        for (int w = w0; w < we; ++w) {
+          const float v = pl[h * Wp + w];
+          if (v > m || __builtin_isnan(v)) m = v;
+        }
+      yn[cc * OHW + q] = m;
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1710,6 +1937,106 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
                      static_cast<hipStream_t>(stream), x, x_kstride, params, params_kstride,
                      w_off, b_off, M, in, out, y, n_tiles, m_tiles,
                      (flags & FEDAGG_RELU) ? 1 : 0);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_conv_stage(int64_t R) {
+  // reductions per LDS stage: 16 when that pads R less (conv1 of the reference's
+  // CNNs: R = 3 * 5 * 5 = 75 -> 80 instead of 96), else 32
+  if (R <= 0) return 0;
+  return ((R + 15) / 16 * 16 < (R + 31) / 32 * 32) ? 16 : 32;
+}
+
+int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* params,
+                              int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t K,
+                              const fedagg_conv2d_shape* shape, float* y, int flags,
+                              void* stream) {
+  if (!shape || K < 0 || x_kstride < 0 || params_kstride < 0 || w_off < 0 || b_off < -1)
+    return FEDAGG_EINVAL;
+  if (flags & ~FEDAGG_RELU) return FEDAGG_EINVAL;
+  const fedagg_conv2d_shape s = *shape;
+  const int64_t lim = int64_t(1) << 15;
+  if (s.M < 0 || s.C <= 0 || s.H <= 0 || s.W <= 0 || s.OC <= 0 || s.KH <= 0 || s.KW <= 0 ||
+      s.stride_h <= 0 || s.stride_w <= 0 || s.pad_h < 0 || s.pad_w < 0 || s.OH <= 0 || s.OW <= 0)
+    return FEDAGG_EINVAL;
+  if (s.H >= lim || s.W >= lim || s.KH >= lim || s.KW >= lim || s.stride_h >= lim ||
+      s.stride_w >= lim || s.pad_h >= lim || s.pad_w >= lim || s.OH >= lim || s.OW >= lim ||
+      s.H * s.W >= (int64_t(1) << 31))
+    return FEDAGG_EINVAL;
+  // every output window must start inside the padded input
+  if ((s.OH - 1) * s.stride_h - s.pad_h >= s.H || (s.OW - 1) * s.stride_w - s.pad_w >= s.W)
+    return FEDAGG_EINVAL;
+  const int64_t R = s.C * s.KH * s.KW;
+  if (K > 1 && (w_off + s.OC * R > params_kstride || (b_off >= 0 && b_off + s.OC > params_kstride)))
+    return FEDAGG_EINVAL;
+  if (K == 0 || s.M == 0) return 0;
+  if (!x || !params || !y) return FEDAGG_EINVAL;
+  const int64_t oc_tiles = (s.OC + kTC_OC - 1) / kTC_OC;
+  const int64_t px_tiles = (s.M * s.OH * s.OW + kTC_PX - 1) / kTC_PX;
+  const int64_t tiles = K * oc_tiles * px_tiles;
+  if (tiles > (int64_t(1) << 31) - 1) return FEDAGG_EINVAL;
+  const int relu = (flags & FEDAGG_RELU) ? 1 : 0;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (fedagg_conv_stage(R) == 16)
+    hipLaunchKernelGGL(k_teacher_conv2d<16>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st,
+                       x, x_kstride, params, params_kstride, w_off, b_off, s, y, oc_tiles,
+                       px_tiles, relu);
+  else
+    hipLaunchKernelGGL(k_teacher_conv2d<32>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st,
+                       x, x_kstride, params, params_kstride, w_off, b_off, s, y, oc_tiles,
+                       px_tiles, relu);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_pool_output(const fedagg_pool_args* a, int64_t* OH, int64_t* OW, int64_t* CB) {
+  if (!a || !OH || !OW || !CB) return FEDAGG_EINVAL;
+  const int64_t lim = int64_t(1) << 15;
+  if (a->N < 0 || a->C <= 0 || a->H <= 0 || a->W <= 0 || a->pad_top < 0 || a->pad_bottom < 0 ||
+      a->pad_left < 0 || a->pad_right < 0 || a->lrn_size < 0 || a->lrn_size >= lim)
+    return FEDAGG_EINVAL;
+  const int64_t Hp = a->H + a->pad_top + a->pad_bottom, Wp = a->W + a->pad_left + a->pad_right;
+  if (Hp >= lim || Wp >= lim || a->C >= (int64_t(1) << 30)) return FEDAGG_EINVAL;
+  int64_t kh = a->pool_kh, kw = a->pool_kw, sh = a->pool_sh, sw = a->pool_sw;
+  int64_t ph = a->pool_ph, pw = a->pool_pw;
+  if (kh == 0) {  // no pooling: the padded, normalised planes themselves
+    kh = kw = sh = sw = 1;
+    ph = pw = 0;
+  }
+  if (kh <= 0 || kw <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0 || 2 * ph > kh || 2 * pw > kw ||
+      kh >= lim || kw >= lim || sh >= lim || sw >= lim)
+    return FEDAGG_EINVAL;
+  if (Hp + 2 * ph < kh || Wp + 2 * pw < kw) return FEDAGG_EINVAL;
+  *OH = (Hp + 2 * ph - kh) / sh + 1;
+  *OW = (Wp + 2 * pw - kw) / sw + 1;
+  // channels per workgroup: their padded planes fit 32 KiB of LDS, balanced over the blocks
+  const int64_t plane = Hp * Wp;
+  if (plane > 16384) return FEDAGG_EINVAL;
+  int64_t cb = 8192 / plane;
+  if (cb < 1) cb = 1;
+  if (cb > a->C) cb = a->C;
+  const int64_t nblk = (a->C + cb - 1) / cb;
+  *CB = (a->C + nblk - 1) / nblk;
+  return 0;
+}
+
+int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, float* y,
+                               void* stream) {
+  int64_t OH = 0, OW = 0, CB = 0;
+  const int rc = fedagg_pool_output(args, &OH, &OW, &CB);
+  if (rc) return rc;
+  fedagg_pool_args a = *args;
+  if (a.pool_kh == 0) {
+    a.pool_kh = a.pool_kw = a.pool_sh = a.pool_sw = 1;
+    a.pool_ph = a.pool_pw = 0;
+  }
+  if (a.N == 0) return 0;
+  if (!x || !y) return FEDAGG_EINVAL;
+  const int64_t blocks = a.N * ((a.C + CB - 1) / CB);
+  if (blocks > (int64_t(1) << 31) - 1) return FEDAGG_EINVAL;
+  const int64_t Hp = a.H + a.pad_top + a.pad_bottom, Wp = a.W + a.pad_left + a.pad_right;
+  const size_t lds = static_cast<size_t>(CB * Hp * Wp) * sizeof(float);
+  hipLaunchKernelGGL(k_pad_lrn_maxpool, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
+                     static_cast<hipStream_t>(stream), x, a, CB, OH, OW, y);
   return static_cast<int>(hipGetLastError());
 }
 

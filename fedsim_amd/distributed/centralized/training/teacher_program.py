@@ -10,11 +10,18 @@ slab of their flat vectors (parameters_to_vector layout):
   launch (``fedagg_teacher_linear_f32``: v_mfma_f32_16x16x4_f32, each
   teacher's weights read once per 64 samples), with a following ReLU fused
   into its epilogue;
-* each maximal run of the other nodes between them (convolutions, pooling,
-  normalisation, reshapes) is ONE ``torch.vmap`` over the teacher dimension,
-  so the convolutional part costs what the whole-model ``vmap`` costs; a run
-  that does not depend on the teachers (the input's own preprocessing) runs
-  once, unbatched.
+* every ``nn.Conv2d`` (groups 1, dilation 1, zero padding) is one implicit-GEMM
+  launch for all K teachers (``fedagg_teacher_conv2d_f32``:
+  v_mfma_f32_32x32x2_f32, the im2col gathered into LDS, never stored), a
+  following ReLU fused;
+* every chain of zero ``F.pad`` / ``local_response_norm`` / ``max_pool2d``
+  after it (the reference's SimpleCNN / SimpleCNN2, simple_models.py:156-159,
+  245-252) is one pass (``fedagg_pad_lrn_maxpool_f32``);
+* each maximal run of the other nodes between them (reshapes, other layers)
+  is ONE ``torch.vmap`` over the teacher dimension; a run that does not
+  depend on the teachers (the input's own preprocessing) runs once, unbatched.
+  A conv or pool node whose runtime shapes the kernels do not take runs the
+  same way.
 
 ``build`` returns None when the model does not trace, so the caller keeps
 its whole-model ``vmap`` path; the ensemble also checks the replay against
@@ -31,7 +38,92 @@ from torch.func import functional_call
 
 from .... import ops
 
-_RELU_FUNCS = (torch.relu, torch.nn.functional.relu)
+F = torch.nn.functional
+_RELU_FUNCS = (torch.relu, F.relu)
+
+
+def _bind(node, names, defaults):
+    """The node's arguments after its input, by name (positional, then
+    keyword, then the defaults); None when it passes unknown ones."""
+    vals = dict(defaults)
+    if len(node.args) - 1 > len(names):
+        return None
+    for n, v in zip(names, node.args[1:]):
+        vals[n] = v
+    for n, v in node.kwargs.items():
+        if n not in names:
+            return None
+        vals[n] = v
+    if any(isinstance(v, torch.fx.Node) for v in vals.values()) or any(
+            n not in vals for n in names):
+        return None
+    return vals
+
+
+def _pair(v):
+    return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
+
+
+def _pool_item(node, modules):
+    """("pad", (top, bottom, left, right)) / ("lrn", (size, alpha, beta, k)) /
+    ("pool", (kh, kw, sh, sw, ph, pw)) for a node fedagg_pad_lrn_maxpool_f32
+    can run, else None."""
+    if node.op == "call_function" and node.target is F.pad:
+        a = _bind(node, ("pad", "mode", "value"), {"mode": "constant", "value": None})
+        if a is None or a["mode"] != "constant" or a["value"] not in (None, 0, 0.0):
+            return None
+        pad = a["pad"]
+        if not isinstance(pad, (tuple, list)) or len(pad) not in (2, 4) or any(
+                not isinstance(v, int) or v < 0 for v in pad):
+            return None
+        pad = tuple(pad) + (0, 0) * (len(pad) == 2)
+        return ("pad", (pad[2], pad[3], pad[0], pad[1]))
+    if node.op == "call_function" and node.target is F.local_response_norm:
+        a = _bind(node, ("size", "alpha", "beta", "k"), {"alpha": 1e-4, "beta": 0.75, "k": 1.0})
+        if a is None or not isinstance(a["size"], int) or a["size"] <= 0:
+            return None
+        return ("lrn", (a["size"], float(a["alpha"]), float(a["beta"]), float(a["k"])))
+    if node.op == "call_function" and node.target is F.max_pool2d:
+        a = _bind(node, ("kernel_size", "stride", "padding", "dilation", "ceil_mode",
+                         "return_indices"),
+                  {"stride": None, "padding": 0, "dilation": 1, "ceil_mode": False,
+                   "return_indices": False})
+    elif node.op == "call_module" and len(node.args) == 1 and not node.kwargs:
+        mod = modules.get(node.target)
+        if type(mod) is nn.MaxPool2d:
+            a = dict(kernel_size=mod.kernel_size, stride=mod.stride, padding=mod.padding,
+                     dilation=mod.dilation, ceil_mode=mod.ceil_mode,
+                     return_indices=mod.return_indices)
+        elif type(mod) is nn.LocalResponseNorm:
+            return ("lrn", (int(mod.size), float(mod.alpha), float(mod.beta), float(mod.k)))
+        elif type(mod) in (nn.ZeroPad2d, nn.ConstantPad2d) and getattr(mod, "value", 0) == 0:
+            l, r, t, b = mod.padding
+            return ("pad", (t, b, l, r))
+        else:
+            return None
+    else:
+        return None
+    if a is None or a["ceil_mode"] or a["return_indices"] or _pair(a["dilation"]) != (1, 1):
+        return None
+    kh, kw = _pair(a["kernel_size"])
+    sh, sw = _pair(a["stride"]) if a["stride"] not in (None, (), []) else (kh, kw)
+    ph, pw = _pair(a["padding"])
+    return ("pool", (kh, kw, sh, sw, ph, pw))
+
+
+def _conv_geometry(mod):
+    """(kernel, stride, (top, bottom, left, right)) of an nn.Conv2d the conv
+    kernel runs (groups 1, dilation 1, zero padding), else None."""
+    if (type(mod) is not nn.Conv2d or mod.groups != 1 or tuple(mod.dilation) != (1, 1)
+            or mod.padding_mode != "zeros"):
+        return None
+    if isinstance(mod.padding, str):
+        l, r, t, b = ((0, 0, 0, 0) if mod.padding == "valid"
+                      else tuple(mod._reversed_padding_repeated_twice))
+    else:
+        t = b = int(mod.padding[0])
+        l = r = int(mod.padding[1])
+    return tuple(mod.kernel_size), tuple(mod.stride), (t, b, l, r)
 
 
 def _is_relu(node, modules) -> bool:
@@ -45,27 +137,31 @@ def _is_relu(node, modules) -> bool:
 
 
 class _Segment(object):
-    """A run of graph nodes replayed by one vmap (kind "ops") or one Linear
-    layer on the matrix cores (kind "linear")."""
+    """A run of graph nodes replayed by one vmap (kind "ops"), one Linear or
+    Conv2d layer on the matrix cores (kind "linear" / "conv"), or one
+    pad / LRN / max-pool chain (kind "pool")."""
 
-    __slots__ = ("kind", "nodes", "inputs", "outputs", "params", "fn")
+    __slots__ = ("kind", "nodes", "inputs", "outputs", "params", "fn", "spec")
 
-    def __init__(self, kind, nodes):
+    def __init__(self, kind, nodes, spec=None):
         self.kind = kind
         self.nodes = nodes
         self.inputs: List = []   # nodes outside the run that it reads
         self.outputs: List = []  # nodes of the run read after it
         self.params: List = []   # parameter names the run reads
-        self.fn = None           # the run as generated code (kind "ops")
+        self.fn = None           # the run as generated code (kind "ops"; the
+        #                          fallback of "conv" / "pool")
+        self.spec = spec         # conv geometry / pool chain
 
 
 class TeacherProgram(object):
     """``program(x)`` = the K teachers' outputs on input ``x``, [K, ...]."""
 
-    def __init__(self, model: nn.Module, named, slab: torch.Tensor, linear=None):
-        # linear: TEST HOOK replacing ops.teacher_linear (same signature), so
-        # the graph replay can be checked on the CPU
-        self.linear_impl = ops.teacher_linear if linear is None else linear
+    def __init__(self, model: nn.Module, named, slab: torch.Tensor, impl=None):
+        # impl: TEST HOOK replacing the ops module (its teacher_linear /
+        # teacher_conv2d / pad_lrn_maxpool, same signatures), so the graph
+        # replay can be checked on the CPU
+        self.impl = ops if impl is None else impl
         self.gm = torch.fx.symbolic_trace(model)
         self.modules = dict(self.gm.named_modules())
         self.slab = slab
@@ -78,36 +174,81 @@ class TeacherProgram(object):
         nodes = list(self.gm.graph.nodes)
         self.placeholders = [n for n in nodes if n.op == "placeholder"]
         self.output = [n for n in nodes if n.op == "output"][0]
-        # a ReLU whose input is a Linear node used only by it: fused
+        # a ReLU whose input is a Linear / Conv2d node used only by it: fused
         self.fused = set()
         self.alias = {}
         for node in nodes:
             if _is_relu(node, self.modules):
                 src = node.args[0]
-                if (src.op == "call_module" and type(self.modules.get(src.target)) is nn.Linear
+                if (isinstance(src, torch.fx.Node) and (self._is_linear(src) or self._is_conv(src))
                         and len(src.users) == 1):
                     self.fused.add(src)
                     self.alias[node] = src
         self.segments = self._partition(nodes)
         self.linear_launches = 0
+        self.conv_launches = 0
+        self.pool_launches = 0
 
     def _is_linear(self, node) -> bool:
         return (node.op == "call_module" and type(self.modules.get(node.target)) is nn.Linear
                 and len(node.args) == 1 and not node.kwargs)
 
+    def _is_conv(self, node) -> bool:
+        return (node.op == "call_module" and len(node.args) == 1 and not node.kwargs
+                and _conv_geometry(self.modules.get(node.target)) is not None)
+
+    def _pool_chain(self, node):
+        """The longest chain from ``node`` of pads, at most one LRN and at
+        most one max pool (ending it), each node feeding only the next:
+        (nodes, pads, lrn, pool), or None."""
+        nodes, pads, lrn, pool = [], [0, 0, 0, 0], None, None
+        cur = node
+        while True:
+            item = _pool_item(cur, self.modules)
+            if item is None or (item[0] == "lrn" and lrn is not None):
+                break
+            nodes.append(cur)
+            if item[0] == "pad":
+                pads = [p + q for p, q in zip(pads, item[1])]
+            elif item[0] == "lrn":
+                lrn = item[1]
+            else:
+                pool = item[1]
+                break
+            users = list(cur.users)
+            if len(users) != 1 or not users[0].args or users[0].args[0] is not cur:
+                break
+            cur = users[0]
+        if not nodes:
+            return None
+        return nodes, tuple(pads), lrn, pool
+
     def _partition(self, nodes):
         segs = []
         run = []
+        taken = set()
+
+        def special(seg):
+            nonlocal run
+            if run:
+                segs.append(_Segment("ops", run))
+                run = []
+            segs.append(seg)
+
         for node in nodes:
-            if node.op in ("placeholder", "output") or node in self.alias:
+            if node.op in ("placeholder", "output") or node in self.alias or node in taken:
                 continue
             if self._is_linear(node):
-                if run:
-                    segs.append(_Segment("ops", run))
-                    run = []
-                segs.append(_Segment("linear", [node]))
+                special(_Segment("linear", [node]))
+            elif self._is_conv(node):
+                special(_Segment("conv", [node], _conv_geometry(self.modules[node.target])))
             else:
-                run.append(node)
+                chain = self._pool_chain(node)
+                if chain is not None:
+                    taken.update(chain[0])
+                    special(_Segment("pool", chain[0], chain[1:]))
+                else:
+                    run.append(node)
         if run:
             segs.append(_Segment("ops", run))
         resolve = lambda n: self.alias.get(n, n)  # noqa: E731
@@ -134,7 +275,7 @@ class TeacherProgram(object):
             if name not in self.offs:
                 raise KeyError(f"parameter {name} is not in the flat vector layout")
         for seg in segs:
-            if seg.kind == "ops":
+            if seg.kind in ("ops", "conv", "pool"):
                 seg.fn = self._compile(seg)
         return segs
 
@@ -174,10 +315,44 @@ class TeacherProgram(object):
         b = self.offs[node.target + ".bias"][0] if mod.bias is not None else -1
         x = value.contiguous().float()
         lead = x.shape[1:-1] if batched else x.shape[:-1]
-        y = self.linear_impl(x, self.slab, w, b, mod.in_features, mod.out_features,
-                             shared=not batched, relu=node in self.fused)
+        y = self.impl.teacher_linear(x, self.slab, w, b, mod.in_features, mod.out_features,
+                                     shared=not batched, relu=node in self.fused)
         self.linear_launches += 1
         return y.view(self.K, *lead, mod.out_features)
+
+    def _conv(self, seg, env) -> bool:
+        """The conv node on the matrix cores; False when its runtime input is
+        not the 4-D (per teacher) f32 image batch the kernel takes."""
+        node = seg.nodes[0]
+        v, batched = env[seg.inputs[0]]
+        if (not isinstance(v, torch.Tensor) or v.dtype != torch.float32
+                or v.dim() != (5 if batched else 4)):
+            return False
+        mod = self.modules[node.target]
+        kernel, stride, pads = seg.spec
+        w = self.offs[node.target + ".weight"][0]
+        b = self.offs[node.target + ".bias"][0] if mod.bias is not None else -1
+        y = self.impl.teacher_conv2d(v.contiguous(), self.slab, w, b, mod.out_channels, kernel,
+                                     stride, pads, shared=not batched, relu=node in self.fused)
+        self.conv_launches += 1
+        env[node] = (y, True)
+        return True
+
+    def _pool(self, seg, env) -> bool:
+        """The pad / LRN / max-pool chain in one pass; False when its runtime
+        input is not a 4-D (per teacher) f32 image batch the kernel takes."""
+        v, batched = env[seg.inputs[0]]
+        if (not isinstance(v, torch.Tensor) or v.dtype != torch.float32
+                or v.dim() != (5 if batched else 4)):
+            return False
+        pads, lrn, pool = seg.spec
+        try:  # ValueError: a shape the kernel does not take (checked before any launch)
+            y = self.impl.pad_lrn_maxpool(v.contiguous(), pads, lrn, pool)
+        except ValueError:
+            return False
+        self.pool_launches += 1
+        env[seg.nodes[-1]] = (y, batched)
+        return True
 
     def _run_ops(self, seg, env):
         vals = [env[n][0] for n in seg.inputs]
@@ -192,16 +367,41 @@ class TeacherProgram(object):
         for o, v in zip(seg.outputs, outs):
             if not isinstance(v, torch.Tensor):
                 raise NotImplementedError("a non-tensor value crosses a Linear layer")
+            if o in self.fused:  # a conv run here: its fused ReLU is not in the run's code
+                v = torch.relu(v)
             env[o] = (v, True)
+
+    # teachers per replay pass: bounds the activations (SimpleCNN2's first
+    # conv output is 9.4 MB per teacher per 64-sample batch)
+    max_teachers = 512
 
     @torch.no_grad()
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if self.K <= self.max_teachers:
+            return self._replay(x)
+        full, K = self.slab, self.K
+        step = -(-K // -(-K // self.max_teachers))
+        outs = []
+        try:
+            for k0 in range(0, K, step):
+                self.slab = full[k0:k0 + step]
+                self.K = self.slab.shape[0]
+                outs.append(self._replay(x))
+        finally:
+            self.slab, self.K = full, K
+        return torch.cat(outs)
+
+    def _replay(self, x: torch.Tensor) -> torch.Tensor:
         env = {p: (x, False) for p in self.placeholders}
         for seg in self.segments:
             if seg.kind == "linear":
                 node = seg.nodes[0]
                 v, b = env[self.alias.get(node.args[0], node.args[0])]
                 env[node] = (self._linear(node, v, b), True)
+            elif seg.kind == "conv" and self._conv(seg, env):
+                pass
+            elif seg.kind == "pool" and self._pool(seg, env):
+                pass
             else:
                 self._run_ops(seg, env)
         res = self.output.args[0]
@@ -211,14 +411,14 @@ class TeacherProgram(object):
         return v
 
 
-def build(model: nn.Module, named, slab: torch.Tensor, linear=None) -> Optional[TeacherProgram]:
+def build(model: nn.Module, named, slab: torch.Tensor, impl=None) -> Optional[TeacherProgram]:
     """A TeacherProgram for ``model``, or None when its forward does not trace,
     uses parameters outside its own ``named_parameters`` layout, or has no
-    Linear layer for the matrix cores to run."""
+    Linear / Conv2d layer for the matrix cores to run."""
     try:
-        prog = TeacherProgram(model, named, slab, linear)
+        prog = TeacherProgram(model, named, slab, impl)
     except Exception:  # noqa: BLE001 - untraceable forward: the caller keeps vmap
         return None
-    if not any(s.kind == "linear" for s in prog.segments):
+    if not any(s.kind in ("linear", "conv") for s in prog.segments):
         return None
     return prog

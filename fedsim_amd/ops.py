@@ -405,6 +405,85 @@ def teacher_linear(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int, 
     return y
 
 
+def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
+                   out_channels: int, kernel_size, stride, padding, shared: bool,
+                   relu: bool = False) -> torch.Tensor:
+    """One nn.Conv2d (groups 1, dilation 1, zero padding) of the K teachers
+    whose flat parameter vectors are the rows of ``slab`` ([K, P]), as an
+    implicit GEMM on the matrix cores (fedagg_teacher_conv2d_f32).  ``x``:
+    [M, C, H, W] shared by every teacher (``shared``) or [K, M, C, H, W].
+    ``padding`` = (top, bottom, left, right) zeros.  Returns
+    y [K, M, OC, OH, OW] (ReLU applied when ``relu``).  b_off = -1: no bias."""
+    _require_hip_f32(x, "x")
+    _require_hip_f32(slab, "slab")
+    if slab.dim() != 2 or not slab.is_contiguous() or x.device != slab.device:
+        raise ValueError("slab must be a contiguous [K, P] tensor on x's device")
+    K, P = slab.shape
+    if not x.is_contiguous() or x.dim() != (4 if shared else 5):
+        raise ValueError("x must be a contiguous [M, C, H, W] (shared) or [K, M, C, H, W] tensor")
+    if not shared and x.shape[0] != K:
+        raise ValueError("a per-teacher x must have K rows in its first dimension")
+    M, C, H, W = x.shape[-4:]
+    KH, KW = kernel_size
+    sh, sw = stride
+    pt, pb, pl, pr = padding
+    OH = (H + pt + pb - KH) // sh + 1
+    OW = (W + pl + pr - KW) // sw + 1
+    if OH <= 0 or OW <= 0:
+        raise ValueError("the padded input is smaller than the kernel")
+    R = C * KH * KW
+    if w_off < 0 or w_off + out_channels * R > P or (b_off >= 0 and b_off + out_channels > P):
+        raise ValueError("layer offsets outside the parameter vector")
+    shape = _native.Conv2dShape(M, C, H, W, out_channels, KH, KW, sh, sw, pt, pl, OH, OW)
+    y = torch.empty((K, M, out_channels, OH, OW), dtype=torch.float32, device=x.device)
+    rc = _native.load().fedagg_teacher_conv2d_f32(
+        x.data_ptr(), 0 if shared else M * C * H * W, slab.data_ptr(), P, w_off, b_off, K,
+        ctypes.byref(shape), y.data_ptr(), _native.FEDAGG_RELU if relu else 0,
+        _stream_ptr(x.device))
+    check(rc, "fedagg_teacher_conv2d_f32")
+    return y
+
+
+def pool_args(shape, pads=(0, 0, 0, 0), lrn=None, pool=None) -> "_native.PoolArgs":
+    """struct fedagg_pool_args for an input of ``shape`` (..., C, H, W):
+    ``pads`` (top, bottom, left, right) zeros, ``lrn`` (size, alpha, beta, k)
+    or None, ``pool`` (kh, kw, sh, sw, ph, pw) or None."""
+    C, H, W = shape[-3:]
+    N = 1
+    for d in shape[:-3]:
+        N *= int(d)
+    size, alpha, beta, k = lrn if lrn is not None else (0, 0.0, 0.0, 0.0)
+    pk = pool if pool is not None else (0, 0, 0, 0, 0, 0)
+    return _native.PoolArgs(N, C, H, W, *pads, size, alpha, beta, k, *pk)
+
+
+def pool_output(args) -> tuple:
+    """(OH, OW) of fedagg_pad_lrn_maxpool_f32, or raise ValueError when the
+    library rejects the chain's shape (the caller keeps torch for it)."""
+    oh, ow, cb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = _native.load().fedagg_pool_output(ctypes.byref(args), ctypes.byref(oh), ctypes.byref(ow),
+                                           ctypes.byref(cb))
+    if rc != 0:
+        raise ValueError("pad / local_response_norm / max_pool2d chain not supported")
+    return oh.value, ow.value
+
+
+def pad_lrn_maxpool(x: torch.Tensor, pads=(0, 0, 0, 0), lrn=None, pool=None) -> torch.Tensor:
+    """F.pad (zeros) -> F.local_response_norm -> F.max_pool2d over the last
+    three dimensions (C, H, W) of ``x`` in one pass
+    (fedagg_pad_lrn_maxpool_f32); leading dimensions are images."""
+    _require_hip_f32(x, "x")
+    if not x.is_contiguous() or x.dim() < 3:
+        raise ValueError("x must be a contiguous (..., C, H, W) tensor")
+    args = pool_args(x.shape, pads, lrn, pool)
+    OH, OW = pool_output(args)
+    y = torch.empty((*x.shape[:-2], OH, OW), dtype=torch.float32, device=x.device)
+    rc = _native.load().fedagg_pad_lrn_maxpool_f32(x.data_ptr(), ctypes.byref(args), y.data_ptr(),
+                                                   _stream_ptr(x.device))
+    check(rc, "fedagg_pad_lrn_maxpool_f32")
+    return y
+
+
 def finalize(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = fl32(acc / fl32(W)) — SerialAggregator.pop's true division."""
     _require_hip_f32(acc, "acc")

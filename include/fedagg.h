@@ -188,6 +188,70 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
                               void* stream);
 
 /*
+ * FedDF's teacher ensemble, convolutional layers (the same feddf.py:117-122
+ * forwards; fedsim/models/simple_models.py:156-158, 245-249 are the
+ * reference's nn.Conv2d layers): ONE nn.Conv2d (groups 1, dilation 1, zero
+ * padding) of K stacked teachers as an implicit GEMM on the matrix cores
+ * (v_mfma_f32_32x32x2_f32):
+ *   y[k][m][oc][oh][ow] = act(b_k[oc] + sum_{c,kh,kw} W_k[oc][c][kh][kw] *
+ *                             x_k[m][c][oh*stride_h - pad_h + kh][ow*stride_w - pad_w + kw])
+ * with out-of-range input positions reading 0 (bottom / right padding is
+ * implied by OH / OW, so torch's asymmetric padding="same" for even kernels
+ * fits).  x_k = x + k*x_kstride ([M, C, H, W] contiguous; x_kstride = 0: one
+ * input shared by all teachers); W_k = params + k*params_kstride + w_off
+ * ([OC, C, KH, KW] row-major, the teacher's flat vector); b_off = -1: no
+ * bias.  y is [K, M, OC, OH, OW] contiguous.  flags: FEDAGG_RELU.  Each
+ * output is the exact f32 fmaf chain over r = (c, kh, kw) in order from
+ * +0.0f, then one bias add: normwise, not bitwise, equal to a CPU conv.
+ */
+typedef struct fedagg_conv2d_shape {
+  int64_t M, C, H, W;          /* per-teacher input [M, C, H, W]            */
+  int64_t OC, KH, KW;          /* output channels, kernel size              */
+  int64_t stride_h, stride_w;  /* >= 1                                      */
+  int64_t pad_h, pad_w;        /* top / left zero padding                   */
+  int64_t OH, OW;              /* output size                               */
+} fedagg_conv2d_shape;
+
+int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* params,
+                              int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t K,
+                              const fedagg_conv2d_shape* shape, float* y, int flags,
+                              void* stream);
+
+/* Reductions per LDS stage the conv kernel takes for R = C*KH*KW (16 or 32;
+ * the exact chain is the same either way). Host-side, no device access. */
+int fedagg_conv_stage(int64_t R);
+
+/*
+ * The memory-bound chain after a convolution of the reference's CNNs
+ * (simple_models.py:246-248, 250-252: F.pad(x, (0, 1, 0, 1)) ->
+ * F.local_response_norm(size 4, alpha 1e-3/9) -> F.max_pool2d(3, 2); :157,
+ * :159 max_pool2d(2, 2, padding 1)) in ONE pass over x [N, C, H, W]:
+ *   1. zero padding (pad_top / bottom / left / right, F.pad's constant 0);
+ *   2. lrn_size > 0: local_response_norm across channels with ATen's
+ *      roundings (window [c - size/2, c + (size-1)/2], zeros outside):
+ *      s = sum fl32(x*x) in channel order from +0, avg = s / size,
+ *      d = powf(fl32(fl32(avg * alpha) + k), beta), v = x / d;
+ *   3. pool_kh > 0: max_pool2d (kernel pool_kh x pool_kw, stride pool_sh x
+ *      pool_sw, implicit -inf padding pool_ph / pool_pw <= half the kernel,
+ *      floor mode, NaN propagates).  pool_kh = 0: no pooling.
+ * Zero padding and LRN commute (LRN(0) = 0), so pad -> LRN and LRN -> pad
+ * are both this call.  y is [N, C, OH, OW] contiguous; fedagg_pool_output
+ * gives OH / OW (and the channels per workgroup).
+ */
+typedef struct fedagg_pool_args {
+  int64_t N, C, H, W;
+  int64_t pad_top, pad_bottom, pad_left, pad_right;
+  int64_t lrn_size;
+  float lrn_alpha, lrn_beta, lrn_k;
+  int64_t pool_kh, pool_kw, pool_sh, pool_sw, pool_ph, pool_pw;
+} fedagg_pool_args;
+
+int fedagg_pool_output(const fedagg_pool_args* args, int64_t* OH, int64_t* OW, int64_t* CB);
+
+int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, float* y,
+                               void* stream);
+
+/*
  * vectorize_module straight into a slab row (fedsim/utils/convert_parameters.py
  * :78-94, parameters_to_vector + the clone at training/utils.py:34): write
  * the concatenation of nseg device segments into row r of a column-blocked

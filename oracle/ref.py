@@ -47,9 +47,12 @@ def lib():
                                           f32, ci, ci, i64]
         L.ref_teacher_linear_f32.argtypes = [vp, i64, vp, i64, i64, i64, i64, i64, i64, i64,
                                              vp, ci]
+        L.ref_teacher_conv2d_f32.argtypes = [vp, i64, vp, i64, i64, i64, i64] + [i64] * 13 + [
+            vp, ci]
+        L.ref_pad_lrn_maxpool_f32.argtypes = [vp] + [i64] * 9 + [f32] * 3 + [i64] * 6 + [vp]
         for fn in ("ref_reduce_f32", "ref_finalize_f32", "ref_fedavg_sgd_f32",
                    "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32", "ref_server_step_f32",
-                   "ref_teacher_linear_f32"):
+                   "ref_teacher_linear_f32", "ref_teacher_conv2d_f32", "ref_pad_lrn_maxpool_f32"):
             getattr(L, fn).restype = None
         _lib = L
     return _lib
@@ -188,4 +191,45 @@ def teacher_linear(x: np.ndarray, slab: np.ndarray, w_off: int, b_off: int, in_f
     y = np.empty((K, M, out_f), dtype=np.float32)
     lib().ref_teacher_linear_f32(_p(x), 0 if shared else M * in_f, _p(slab), P, w_off, b_off,
                                  K, M, in_f, out_f, _p(y), int(relu))
+    return y
+
+
+def teacher_conv2d(x: np.ndarray, slab: np.ndarray, w_off: int, b_off: int, out_channels: int,
+                   kernel_size, stride, padding, shared: bool, relu: bool = False) -> np.ndarray:
+    """C oracle of fedagg_teacher_conv2d_f32 (the fmaf chain over
+    (c, kh, kw) in order; see fedagg_ref.c).  padding = (top, bottom, left,
+    right); returns [K, M, OC, OH, OW]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    slab = np.ascontiguousarray(slab, dtype=np.float32)
+    K, P = slab.shape
+    M, C, H, W = x.shape[-4:]
+    KH, KW = kernel_size
+    sh, sw = stride
+    pt, pb, pl, pr = padding
+    OH = (H + pt + pb - KH) // sh + 1
+    OW = (W + pl + pr - KW) // sw + 1
+    y = np.empty((K, M, out_channels, OH, OW), dtype=np.float32)
+    lib().ref_teacher_conv2d_f32(_p(x), 0 if shared else M * C * H * W, _p(slab), P, w_off, b_off,
+                                 K, M, C, H, W, out_channels, KH, KW, sh, sw, pt, pl, OH, OW,
+                                 _p(y), int(relu))
+    return y
+
+
+def pad_lrn_maxpool(x: np.ndarray, pads=(0, 0, 0, 0), lrn=None, pool=None) -> np.ndarray:
+    """C oracle of fedagg_pad_lrn_maxpool_f32 over the last three dimensions
+    (C, H, W) of x: zero pads (top, bottom, left, right), lrn (size, alpha,
+    beta, k) or None, pool (kh, kw, sh, sw, ph, pw) or None."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    C, H, W = x.shape[-3:]
+    N = x.size // (C * H * W) if x.size else 0
+    size, alpha, beta, k = lrn if lrn is not None else (0, 0.0, 0.0, 0.0)
+    kh, kw, sh, sw, ph, pw = pool if pool is not None else (0, 0, 0, 0, 0, 0)
+    Hp, Wp = H + pads[0] + pads[1], W + pads[2] + pads[3]
+    if kh == 0:
+        OH, OW = Hp, Wp
+    else:
+        OH, OW = (Hp + 2 * ph - kh) // sh + 1, (Wp + 2 * pw - kw) // sw + 1
+    y = np.empty((*x.shape[:-2], OH, OW), dtype=np.float32)
+    lib().ref_pad_lrn_maxpool_f32(_p(x), N, C, H, W, *pads, size, alpha, beta, k, kh, kw, sh, sw,
+                                  ph, pw, _p(y))
     return y

@@ -43,7 +43,9 @@ def test_header_declares_the_abi():
         "fedagg_abi_version", "fedagg_strerror", "fedagg_column_mapping", "fedagg_reduce_f32",
         "fedagg_reduce_rows_f32",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_pack_segments_f32",
-        "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_finalize_f32",
+        "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_teacher_conv2d_f32",
+        "fedagg_conv_stage", "fedagg_pool_output", "fedagg_pad_lrn_maxpool_f32",
+        "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
         "fedagg_reduce_step_blocked_f32", "fedagg_reduce_step_rows_f32",
@@ -197,3 +199,34 @@ def test_column_mapping_decision():
     assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow1", unroll=16)) == ("narrow1", 16)
     # unroll selectors the narrow kernels do not build fall back to the default
     assert ops.column_mapping(199_210, ops.tuning_flags(unroll=4)) == ("narrow1", 8)
+
+
+def test_conv_and_pool_host_side_shapes(lib):
+    """The host-only helpers of the FedDF conv / pool kernels: the conv's LDS
+    stage depth, and the pool pass's output size (torch's floor-mode
+    max_pool2d formula) and its rejections (no device access)."""
+    import ctypes
+
+    from fedsim_amd import _native, ops
+
+    assert [lib.fedagg_conv_stage(r) for r in (0, 1, 16, 17, 32, 75, 96, 1600)] == \
+        [0, 16, 16, 32, 32, 16, 32, 32]
+    # SimpleCNN2 (simple_models.py:245-252): 24x24 -> pad 25x25 -> pool 3/2 -> 12x12; 12 -> 13 -> 6
+    a = ops.pool_args((64, 64, 24, 24), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0))
+    assert ops.pool_output(a) == (12, 12)
+    a = ops.pool_args((64, 64, 12, 12), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0))
+    assert ops.pool_output(a) == (6, 6)
+    # SimpleCNN (simple_models.py:157): max_pool2d(2, 2, padding=1) on 28x28 -> 15x15
+    assert ops.pool_output(ops.pool_args((1, 32, 28, 28), pool=(2, 2, 2, 2, 1, 1))) == (15, 15)
+    assert ops.pool_output(ops.pool_args((1, 3, 5, 7), (1, 2, 3, 4))) == (8, 14)  # no pool
+    oh, ow, cb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    a = ops.pool_args((8, 64, 24, 24), (0, 1, 0, 1), None, (3, 3, 2, 2, 0, 0))
+    assert lib.fedagg_pool_output(ctypes.byref(a), ctypes.byref(oh), ctypes.byref(ow),
+                                  ctypes.byref(cb)) == 0
+    assert cb.value * 625 * 4 <= 32768 and cb.value >= 1
+    for bad in (ops.pool_args((1, 1, 200, 200)),                         # plane > 64 KiB
+                ops.pool_args((1, 1, 8, 8), pool=(2, 2, 2, 2, 2, 0)),    # padding > kernel / 2
+                ops.pool_args((1, 1, 2, 2), pool=(3, 3, 1, 1, 0, 0)),    # kernel > input
+                ops.pool_args((1, 1, 8, 8), (-1, 0, 0, 0))):
+        assert lib.fedagg_pool_output(ctypes.byref(bad), ctypes.byref(oh), ctypes.byref(ow),
+                                      ctypes.byref(cb)) == _native.FEDAGG_EINVAL

@@ -1,15 +1,19 @@
 """FedDF's teacher ensemble on the matrix cores (fedagg_teacher_linear_f32,
-training/teacher_program.py): the layer kernel against an fp64 reference
-within the f32 dot-product error bound, over ragged shapes; the traced replay
-of whole models (MLP, CNN) over K stacked teachers against each teacher's own
-forward; and the ensemble keeping the kernel path after its first-batch check.
-Reference: fedsim/distributed/centralized/training/feddf.py:117-122."""
+fedagg_teacher_conv2d_f32, fedagg_pad_lrn_maxpool_f32,
+training/teacher_program.py): the layer kernels against an fp64 reference
+within the f32 dot-product error bound and bit for bit against the C
+oracle's fmaf chains, over ragged shapes; the pad / LRN / max-pool pass
+against the C oracle and torch's own ops; the traced replay of whole models
+(MLP, CNNs incl. the reference's SimpleCNN2) over K stacked teachers against
+each teacher's own forward; and the ensemble keeping the kernel path after
+its first-batch check.  Reference: fedsim/distributed/centralized/training/
+feddf.py:117-122, fedsim/models/simple_models.py:165-255."""
 import numpy as np
 import pytest
 import torch
 from torch.func import functional_call
 
-from test_teacher_program import Cnn, Mlp, Tiny
+from test_teacher_program import Cnn, Cnn2, Mlp, Tiny
 
 pytestmark = pytest.mark.gpu
 
@@ -47,7 +51,7 @@ def test_teacher_linear_kernel(M, in_f, out_f, shared, bias, relu):
 
 
 @pytest.mark.parametrize("cls,shape", [(Tiny, (64, 37)), (Mlp, (100, 1, 8, 8)),
-                                       (Cnn, (64, 3, 8, 8))])
+                                       (Cnn, (64, 3, 8, 8)), (Cnn2, (64, 3, 8, 8))])
 def test_program_replays_each_teachers_forward(cls, shape):
     from fedsim_amd.distributed.centralized.training import teacher_program as TP
     from fedsim_amd.utils import vector_to_named_parameters_like
@@ -68,6 +72,8 @@ def test_program_replays_each_teachers_forward(cls, shape):
                 torch.linalg.vector_norm(want.double()))
     assert rel <= 1e-5, rel
     assert prog.linear_launches == sum(isinstance(m, torch.nn.Linear) for m in model.modules())
+    assert prog.conv_launches == sum(isinstance(m, torch.nn.Conv2d) for m in model.modules())
+    assert prog.pool_launches == {Tiny: 0, Mlp: 0, Cnn: 2, Cnn2: 2}[cls]
 
 
 def test_ensemble_keeps_the_matrix_core_path():
@@ -144,3 +150,208 @@ def test_teacher_linear_random_shapes_bitwise():
         exp = ref.teacher_linear(x, slab, w_off, b_off, in_f, out_f, shared, relu)
         np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp),
                                       err_msg=f"K={K} M={M} in={in_f} out={out_f}")
+
+
+# (M, C, H, W, OC, kernel, stride, pads=(top, bottom, left, right))
+CONV_CASES = [
+    (2, 3, 24, 24, 64, (5, 5), (1, 1), (2, 2, 2, 2)),    # SimpleCNN2 conv1 (R = 75: 16-stages)
+    (2, 64, 12, 12, 64, (5, 5), (1, 1), (2, 2, 2, 2)),   # SimpleCNN2 conv2 (R = 1600)
+    (3, 1, 28, 28, 32, (5, 5), (1, 1), (2, 2, 2, 2)),    # SimpleCNN conv1 on MNIST
+    (1, 5, 7, 9, 5, (3, 4), (1, 1), (1, 1, 1, 2)),       # padding="same", even kernel width
+    (4, 7, 11, 10, 100, (3, 3), (2, 2), (1, 1, 1, 1)),   # stride 2, two channel tiles
+    (5, 2, 6, 6, 3, (1, 1), (1, 1), (0, 0, 0, 0)),       # 1x1
+    (1, 33, 5, 5, 65, (5, 5), (1, 3), (0, 0, 4, 0)),     # R = 825, ragged everything
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("shared", [True, False])
+def test_teacher_conv2d_kernel_is_the_fmaf_chain(case, shared):
+    """Bitwise against the C oracle's restatement (oracle/fedagg_ref.c
+    ref_teacher_conv2d_f32): each output is the fmaf chain over (c, kh, kw)
+    in order (zeros outside the input), then one bias add, then ReLU -- the
+    implicit GEMM on v_mfma_f32_32x32x2_f32; and within the f32 dot-product
+    bound of an fp64 convolution."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    M, C, H, W, OC, kern, stride, pads = case
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + C * 13 + OC)
+    K = 3
+    R = C * kern[0] * kern[1]
+    w_off = 5
+    P = w_off + OC * R + OC + 3
+    slab = torch.randn(K, P, device=DEV, generator=g)
+    x = torch.randn((M, C, H, W) if shared else (K, M, C, H, W), device=DEV, generator=g)
+    x.view(-1)[:: 97] = -0.0
+    for bias, relu in ((True, False), (False, True), (True, True)):
+        b_off = w_off + OC * R if bias else -1
+        y = ops.teacher_conv2d(x, slab, w_off, b_off, OC, kern, stride, pads, shared=shared,
+                               relu=relu)
+        exp = ref.teacher_conv2d(x.cpu().numpy(), slab.cpu().numpy(), w_off, b_off, OC, kern,
+                                 stride, pads, shared, relu)
+        assert y.shape == exp.shape
+        np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp))
+    # and the chain is a convolution: fp64 within gamma_R
+    F = torch.nn.functional
+    Wt = slab[:, w_off:w_off + OC * R].view(K, OC, C, *kern).double()
+    bt = slab[:, w_off + OC * R:w_off + OC * R + OC].double()
+    xs = (x.expand(K, *x.shape) if shared else x).double()
+    t, b, l, r = pads
+    y = ops.teacher_conv2d(x, slab, w_off, w_off + OC * R, OC, kern, stride, pads, shared=shared)
+    gamma = (R + 1) * 2.0 ** -24 / (1 - (R + 1) * 2.0 ** -24)
+    for k in range(K):
+        xp = F.pad(xs[k], (l, r, t, b))
+        y64 = F.conv2d(xp, Wt[k], bt[k], stride)
+        absum = F.conv2d(xp.abs(), Wt[k].abs(), bt[k].abs(), stride)
+        err = (y[k].double() - y64).abs()
+        assert bool((err <= gamma * absum + 1e-30).all())
+
+
+def test_teacher_conv2d_random_shapes_bitwise():
+    """Random conv geometries, offsets and teacher counts (seeded), bitwise
+    vs the C oracle, special values in the input included."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    rng = np.random.default_rng(355)
+    for _ in range(30):
+        K = int(rng.integers(1, 4))
+        M = int(rng.integers(1, 4))
+        C = int(rng.integers(1, 20))
+        H, W = int(rng.integers(1, 14)), int(rng.integers(1, 14))
+        kh, kw = int(rng.integers(1, min(H, 5) + 1)), int(rng.integers(1, min(W, 5) + 1))
+        sh, sw = int(rng.integers(1, 3)), int(rng.integers(1, 3))
+        pads = tuple(int(v) for v in rng.integers(0, 3, 4))
+        OC = int(rng.integers(1, 80))
+        R = C * kh * kw
+        w_off = int(rng.integers(0, 7))
+        bias = bool(rng.integers(0, 2))
+        P = w_off + OC * R + (OC if bias else 0) + int(rng.integers(0, 4))
+        slab = rng.standard_normal((K, P)).astype(np.float32)
+        shared = bool(rng.integers(0, 2))
+        x = rng.standard_normal((M, C, H, W) if shared else (K, M, C, H, W)).astype(np.float32)
+        x.reshape(-1)[:: max(1, x.size // 5)] = np.float32(-0.0)
+        relu = bool(rng.integers(0, 2))
+        b_off = w_off + OC * R if bias else -1
+        y = ops.teacher_conv2d(torch.from_numpy(x).to(DEV), torch.from_numpy(slab).to(DEV),
+                               w_off, b_off, OC, (kh, kw), (sh, sw), pads, shared=shared,
+                               relu=relu)
+        exp = ref.teacher_conv2d(x, slab, w_off, b_off, OC, (kh, kw), (sh, sw), pads, shared,
+                                 relu)
+        np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp),
+                                      err_msg=f"K={K} M={M} C={C} HxW={H}x{W} k={kh}x{kw} "
+                                              f"s={sh}x{sw} pads={pads} OC={OC}")
+
+
+# (shape, pads, lrn, pool)
+POOL_CASES = [
+    ((4, 64, 24, 24), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0)),  # SimpleCNN2 1
+    ((4, 64, 12, 12), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0)),  # SimpleCNN2 2
+    ((3, 32, 28, 28), (0, 0, 0, 0), None, (2, 2, 2, 2, 1, 1)),                       # SimpleCNN
+    ((2, 5, 7, 9), (1, 2, 0, 3), (3, 0.01, 0.5, 2.0), None),                         # no pool
+    ((2, 3, 6, 5), (0, 0, 0, 0), (5, 1.0, 1.25, 0.5), (2, 3, 1, 2, 1, 1)),           # C < size
+    ((1, 70, 30, 31), (2, 0, 1, 1), (4, 1e-4, 0.75, 1.0), (3, 2, 3, 2, 1, 0)),       # 2 channels / WG
+]
+
+
+@pytest.mark.parametrize("case", POOL_CASES)
+def test_pad_lrn_maxpool_kernel(case):
+    """Against the C oracle (pooling, padding and the channel window exactly;
+    the LRN's powf within 2 ulps of the host's) and against torch's own
+    F.pad -> F.local_response_norm -> F.max_pool2d on the same GPU."""
+    from fedsim_amd import ops
+    from oracle import ref
+
+    shape, pads, lrn, pool = case
+    g = torch.Generator(device=DEV).manual_seed(sum(shape))
+    x = torch.randn(*shape, device=DEV, generator=g) * 3
+    x.view(-1)[:: 89] = 0.0
+    y = ops.pad_lrn_maxpool(x, pads, lrn, pool)
+    exp = ref.pad_lrn_maxpool(x.cpu().numpy(), pads, lrn, pool)
+    assert y.shape == exp.shape
+    got = y.cpu().numpy()
+    if lrn is None:
+        np.testing.assert_array_equal(got, exp)
+    else:
+        ulp = np.spacing(np.abs(exp).astype(np.float32))
+        assert float((np.abs(got - exp) / ulp).max()) <= 2.0
+    F = torch.nn.functional
+    t, b, l, r = pads
+    want = F.pad(x, (l, r, t, b))
+    if lrn is not None:
+        want = F.local_response_norm(want, lrn[0], alpha=lrn[1], beta=lrn[2], k=lrn[3])
+    if pool is not None:
+        kh, kw, sh, sw, ph, pw = pool
+        want = F.max_pool2d(want, (kh, kw), (sh, sw), (ph, pw))
+    torch.testing.assert_close(y, want, rtol=3e-7, atol=0)
+
+
+def test_pad_lrn_maxpool_special_values():
+    """NaN propagates through the max pool and +-inf through pooling without
+    LRN, as torch's max_pool2d does; 5-D input (teachers x images)."""
+    from fedsim_amd import ops
+
+    x = torch.randn(2, 3, 4, 6, 6, device=DEV)
+    x[0, 1, 2, 3, 3] = float("nan")
+    x[1, 0, 0, 0, 0] = float("inf")
+    x[1, 2, 1, 5, 5] = float("-inf")
+    y = ops.pad_lrn_maxpool(x, (0, 1, 0, 1), None, (3, 3, 2, 2, 0, 0))
+    want = torch.nn.functional.max_pool2d(
+        torch.nn.functional.pad(x.view(6, 4, 6, 6), (0, 1, 0, 1)), 3, 2).view(2, 3, 4, 3, 3)
+    torch.testing.assert_close(y, want, equal_nan=True, rtol=0, atol=0)
+
+
+def test_kernel_shape_guards():
+    """Rejected before any launch: a pool plane above 64 KiB of LDS, a pool
+    padding above half the kernel, and conv layers outside the teacher's
+    vector."""
+    import ctypes
+
+    from fedsim_amd import _native, ops
+
+    x = torch.zeros(1, 1, 200, 200, device=DEV)
+    with pytest.raises(ValueError):
+        ops.pad_lrn_maxpool(x, (0, 0, 0, 0), None, (2, 2, 2, 2, 0, 0))
+    with pytest.raises(ValueError):
+        ops.pad_lrn_maxpool(torch.zeros(1, 1, 8, 8, device=DEV), (0, 0, 0, 0), None,
+                            (2, 2, 2, 2, 2, 2))
+    slab = torch.zeros(2, 10, device=DEV)
+    with pytest.raises(ValueError):
+        ops.teacher_conv2d(torch.zeros(1, 1, 4, 4, device=DEV), slab, 0, -1, 2, (3, 3), (1, 1),
+                           (0, 0, 0, 0), shared=True)
+    shape = _native.Conv2dShape(1, 1, 4, 4, 1, 3, 3, 1, 1, 0, 0, 2, 2)
+    rc = _native.load().fedagg_teacher_conv2d_f32(0, 0, slab.data_ptr(), 10, 5, -1, 2,
+                                                  ctypes.byref(shape), 0, 0, None)
+    assert rc == _native.FEDAGG_EINVAL
+
+
+def test_simplecnn2_replay_at_reference_size():
+    """The reference's SimpleCNN2 (CIFAR-100 head) at its own input size over
+    40 teachers: the replay with both convolutions, both pad / LRN / pool
+    passes and the three Linear layers on this library's kernels matches
+    each teacher's own forward normwise."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    from bench_feddf_teachers import SimpleCNN2
+    from fedsim_amd.distributed.centralized.training import teacher_program as TP
+    from fedsim_amd.utils import vector_to_named_parameters_like
+
+    torch.manual_seed(5)
+    model = SimpleCNN2().to(DEV)
+    named = list(model.named_parameters())
+    K = 40
+    base = torch.cat([p.detach().reshape(-1) for _, p in named])
+    slab = torch.stack([base + 0.05 * torch.randn_like(base) for _ in range(K)])
+    prog = TP.build(model, named, slab)
+    x = torch.randn(64, 3, 24, 24, device=DEV)
+    got = prog(x)
+    want = torch.stack([functional_call(model, vector_to_named_parameters_like(slab[k], named),
+                                        (x,)) for k in range(K)])
+    rel = float(torch.linalg.vector_norm((got - want).double()) /
+                torch.linalg.vector_norm(want.double()))
+    assert rel <= 1e-5, rel
+    assert (prog.conv_launches, prog.pool_launches, prog.linear_launches) == (2, 2, 3)

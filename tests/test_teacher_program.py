@@ -1,9 +1,12 @@
 """FedDF's teacher graph replay (training/teacher_program.py) on the CPU: the
-traced model replayed over K stacked teachers -- Linear layers through the
-layer hook (here a torch stand-in for fedagg_teacher_linear_f32, which the GPU
-test exercises), everything else under vmap -- equals running each teacher's
-own forward.  Reference: fedsim/distributed/centralized/training/
+traced model replayed over K stacked teachers -- Linear / Conv2d layers and
+pad / LRN / max-pool chains through the kernel hook (here torch stand-ins for
+fedagg_teacher_linear_f32 / _conv2d_f32 / fedagg_pad_lrn_maxpool_f32, which
+the GPU tests exercise), everything else under vmap -- equals running each
+teacher's own forward.  Reference: fedsim/distributed/centralized/training/
 feddf.py:117-122 (one forward per teacher per batch)."""
+import types
+
 import pytest
 import torch
 from torch import nn
@@ -21,6 +24,37 @@ def linear_stub(x, slab, w_off, b_off, in_f, out_f, shared, relu=False):
     if b_off >= 0:
         y = y + slab[:, b_off:b_off + out_f].view(K, 1, out_f)
     return torch.relu(y) if relu else y
+
+
+def conv_stub(x, slab, w_off, b_off, oc, kernel, stride, pads, shared, relu=False):
+    K = slab.shape[0]
+    C = x.shape[-3]
+    W = slab[:, w_off:w_off + oc * C * kernel[0] * kernel[1]].view(K, oc, C, *kernel)
+    xs = x.expand(K, *x.shape) if shared else x
+    t, b, l, r = pads
+    ys = []
+    for k in range(K):
+        bias = slab[k, b_off:b_off + oc] if b_off >= 0 else None
+        ys.append(torch.nn.functional.conv2d(torch.nn.functional.pad(xs[k], (l, r, t, b)), W[k],
+                                             bias, stride))
+    y = torch.stack(ys)
+    return torch.relu(y) if relu else y
+
+
+def pool_stub(x, pads, lrn, pool):
+    F = torch.nn.functional
+    t, b, l, r = pads
+    y = F.pad(x.reshape(-1, *x.shape[-3:]), (l, r, t, b))
+    if lrn is not None:
+        y = F.local_response_norm(y, lrn[0], alpha=lrn[1], beta=lrn[2], k=lrn[3])
+    if pool is not None:
+        kh, kw, sh, sw, ph, pw = pool
+        y = F.max_pool2d(y, (kh, kw), (sh, sw), (ph, pw))
+    return y.reshape(*x.shape[:-3], *y.shape[-3:])
+
+
+STUBS = types.SimpleNamespace(teacher_linear=linear_stub, teacher_conv2d=conv_stub,
+                              pad_lrn_maxpool=pool_stub)
 
 
 class Tiny(nn.Module):
@@ -67,7 +101,32 @@ class Cnn(nn.Module):
         return self.cls(h.relu())
 
 
-@pytest.mark.parametrize("cls,shape", [(Tiny, (9, 37)), (Mlp, (7, 1, 8, 8)), (Cnn, (5, 3, 8, 8))])
+class Cnn2(nn.Module):
+    """The reference SimpleCNN2's forward (simple_models.py:244-255) at a
+    small size: conv -> relu -> pad -> LRN -> max pool, twice; and SimpleCNN's
+    max_pool2d(2, 2, padding=1) (simple_models.py:157)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 8, 5, padding="same")
+        self.conv2 = nn.Conv2d(8, 6, (3, 4), padding="same")
+        self.fc = nn.Linear(6 * 3 * 3, 4)
+
+    def forward(self, x):
+        F = torch.nn.functional
+        x = F.relu(self.conv1(x))
+        x = F.pad(x, (0, 1, 0, 1), value=0)
+        x = F.local_response_norm(x, size=4, alpha=0.001 / 9)
+        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=0)
+        x = F.relu(self.conv2(x))
+        x = F.local_response_norm(x, size=4, alpha=0.001 / 9)
+        x = F.pad(x, (0, 1, 0, 1), value=0)
+        x = F.max_pool2d(x, 2, stride=2, padding=1)
+        return self.fc(x.view(x.shape[0], -1))
+
+
+@pytest.mark.parametrize("cls,shape", [(Tiny, (9, 37)), (Mlp, (7, 1, 8, 8)), (Cnn, (5, 3, 8, 8)),
+                                       (Cnn2, (4, 3, 8, 8))])
 def test_replay_equals_per_teacher_forwards(cls, shape):
     torch.manual_seed(0)
     model = cls()
@@ -75,7 +134,7 @@ def test_replay_equals_per_teacher_forwards(cls, shape):
     K = 6
     base = torch.cat([p.detach().reshape(-1) for _, p in named])
     slab = torch.stack([base + 0.1 * torch.randn_like(base) for _ in range(K)])
-    prog = TP.build(model, named, slab, linear=linear_stub)
+    prog = TP.build(model, named, slab, impl=STUBS)
     assert prog is not None
     x = torch.randn(*shape)
     got = prog(x)
@@ -85,12 +144,14 @@ def test_replay_equals_per_teacher_forwards(cls, shape):
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
     n_linear = sum(isinstance(m, nn.Linear) for m in model.modules())
     assert prog.linear_launches == n_linear
+    n_conv = sum(isinstance(m, nn.Conv2d) for m in model.modules())
+    assert prog.conv_launches == n_conv
     # the nodes between Linear layers run as one vmap per run
     kinds = [s.kind for s in prog.segments]
     assert kinds.count("linear") == n_linear
     assert all(not (a == b == "ops") for a, b in zip(kinds, kinds[1:]))
-    # a ReLU right after a Linear used only by it is fused into the layer
-    assert len(prog.fused) == {Tiny: 1, Mlp: 2, Cnn: 1}[cls]
+    # a ReLU right after a Linear / Conv2d used only by it is fused into the layer
+    assert len(prog.fused) == {Tiny: 1, Mlp: 2, Cnn: 2, Cnn2: 2}[cls]
 
 
 def test_untraceable_model_is_refused():
@@ -106,10 +167,73 @@ def test_untraceable_model_is_refused():
 
     m = Dyn()
     slab = torch.zeros(2, sum(p.numel() for p in m.parameters()))
-    assert TP.build(m, list(m.named_parameters()), slab, linear=linear_stub) is None
+    assert TP.build(m, list(m.named_parameters()), slab, impl=STUBS) is None
 
 
-def test_model_without_linear_is_refused():
-    m = nn.Sequential(nn.Conv2d(1, 1, 1))
+def test_model_without_matrix_layers_is_refused():
+    m = nn.Sequential(nn.Conv2d(1, 1, 1, groups=1, dilation=2))
     slab = torch.zeros(2, sum(p.numel() for p in m.parameters()))
-    assert TP.build(m, list(m.named_parameters()), slab, linear=linear_stub) is None
+    assert TP.build(m, list(m.named_parameters()), slab, impl=STUBS) is None
+
+
+def test_pool_chains_are_one_segment_each():
+    """SimpleCNN2's relu -> pad -> LRN -> max pool and LRN -> pad -> max pool
+    chains become one "pool" segment each, with the pads summed."""
+    torch.manual_seed(0)
+    model = Cnn2()
+    named = list(model.named_parameters())
+    slab = torch.stack([torch.cat([p.detach().reshape(-1) for _, p in named])] * 2)
+    prog = TP.build(model, named, slab, impl=STUBS)
+    pools = [s for s in prog.segments if s.kind == "pool"]
+    assert [s.spec for s in pools] == [
+        ((0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0)),
+        ((0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (2, 2, 2, 2, 1, 1))]
+    assert [s.kind for s in prog.segments] == ["conv", "pool", "conv", "pool", "ops", "linear"]
+
+
+def test_conv_and_pool_fall_back_on_shapes_the_kernels_do_not_take():
+    """A pool chain on a 3-D tensor and a conv on an unbatched 3-D input run
+    under vmap (the segment's compiled fallback), with the fused ReLU kept."""
+    class Odd(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(2, 3, 3, padding=1)
+            self.fc = nn.Linear(3 * 4 * 4, 2)
+
+        def forward(self, x):
+            h = torch.relu(self.conv(x[0]))  # 3-D conv input (one unbatched image)
+            h = torch.nn.functional.max_pool2d(h, 2)  # 3-D: not the kernel's layout
+            return self.fc(h.reshape(1, -1))
+
+    torch.manual_seed(3)
+    model = Odd()
+    named = list(model.named_parameters())
+    K = 3
+    base = torch.cat([p.detach().reshape(-1) for _, p in named])
+    slab = torch.stack([base + 0.1 * torch.randn_like(base) for _ in range(K)])
+    prog = TP.build(model, named, slab, impl=STUBS)
+    x = torch.randn(2, 2, 8, 8)
+    got = prog(x)
+    want = torch.stack([functional_call(model, vector_to_named_parameters_like(slab[k], named),
+                                        (x,)) for k in range(K)])
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+    assert prog.conv_launches == 0 and prog.pool_launches == 0
+
+
+def test_replay_in_teacher_chunks():
+    """More teachers than one pass takes: the replay runs over row slices of
+    the slab and concatenates, same outputs as one pass."""
+    torch.manual_seed(4)
+    model = Cnn2()
+    named = list(model.named_parameters())
+    K = 7
+    base = torch.cat([p.detach().reshape(-1) for _, p in named])
+    slab = torch.stack([base + 0.1 * torch.randn_like(base) for _ in range(K)])
+    x = torch.randn(3, 3, 8, 8)
+    whole = TP.build(model, named, slab, impl=STUBS)(x)
+    prog = TP.build(model, named, slab, impl=STUBS)
+    prog.max_teachers = 3
+    got = prog(x)
+    assert prog.K == K and prog.slab is slab
+    assert prog.conv_launches == 2 * 3  # two convs x three passes (3, 3, 1 teachers)
+    torch.testing.assert_close(got, whole, rtol=0, atol=0)

@@ -79,10 +79,15 @@ def timed(fn, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--K", default="10,100,1000")
+    ap.add_argument("--models", default="SimpleMLP,SimpleCNN2")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-vmap", action="store_true", help="time the replay only")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for name, cls, shape in (("SimpleMLP", SimpleMLP, (64, 1, 28, 28)),
                              ("SimpleCNN2", SimpleCNN2, (64, 3, 24, 24))):
+        if name not in a.models.split(","):
+            continue
         torch.manual_seed(0)
         model = cls().to(dev)
         P = sum(p.numel() for p in model.parameters())
@@ -93,13 +98,17 @@ def main():
             ens = TeacherEnsemble(model, teachers, dev)
             ens.mean_logits(x)  # first-batch check
             kept = ens.program is not None
-            t_prog = timed(lambda: ens.mean_logits(x)) if kept else None
-            vm = TeacherEnsemble(model, teachers, dev, program=False)
-            t_vmap = timed(lambda: vm.mean_logits(x))
+            t_prog = timed(lambda: ens.mean_logits(x), a.reps) if kept else None
+            t_vmap = None
+            if not a.no_vmap:
+                vm = TeacherEnsemble(model, teachers, dev, program=False)
+                t_vmap = timed(lambda: vm.mean_logits(x), a.reps)
+                del vm
             print(json.dumps(dict(model=name, P=P, K=K, B=shape[0], program_kept=kept,
                                   matrix_core_ms=t_prog, vmap_ms=t_vmap,
-                                  speedup=(t_vmap / t_prog) if t_prog else None)), flush=True)
-            del ens, vm, teachers
+                                  speedup=(t_vmap / t_prog) if t_prog and t_vmap else None)),
+                  flush=True)
+            del ens, teachers
             torch.cuda.empty_cache()
 
 
