@@ -1565,14 +1565,16 @@ template <int RK>
 __global__ __launch_bounds__(256) void k_teacher_conv2d(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s,
-    float* __restrict__ y, int64_t oc_tiles, int64_t px_tiles, int relu) {
+    float* __restrict__ y, int relu) {
   __shared__ float sW[kTC_OC][RK + kTC_WPAD];
   __shared__ float sX[RK][kTC_PX + kTC_XPAD];
-  const int64_t tile = blockIdx.x;
-  const int64_t k = tile / (oc_tiles * px_tiles);
-  const int64_t rem = tile - k * oc_tiles * px_tiles;
-  const int64_t oc0 = (rem / px_tiles) * kTC_OC;
-  const int64_t px0 = (rem % px_tiles) * kTC_PX;
+  // grid (pixel tiles, channel tiles, teachers): the tile coordinates come
+  // from SGPRs, so the buffer resources below are wave-uniform (a descriptor
+  // derived from a VALU division makes the compiler wrap every load in a
+  // waterfall loop)
+  const int64_t k = blockIdx.z;
+  const int64_t oc0 = int64_t(blockIdx.y) * kTC_OC;
+  const int64_t px0 = int64_t(blockIdx.x) * kTC_PX;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
@@ -1580,12 +1582,21 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
   const int64_t NPX = s.M * OHW;
   const int64_t HW = s.H * s.W;
   const int64_t R = s.C * s.KH * s.KW;
-  const float* wk = params + k * params_kstride + w_off;
+  // the teacher's input and weight matrix as buffer resources: an offset past
+  // num_records (the zero padding, the tails past R / OC / the last pixel)
+  // reads 0 without a branch; per element the address is a 32-bit VGPR
+  // offset, the (c, kh, kw) part of it wave-uniform
+  constexpr uint32_t kOut = 0x80000000u;  // > num_records (host: < 2^31 bytes)
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + k * x_kstride), static_cast<short>(0),
+      static_cast<int>(s.M * s.C * HW * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(params + k * params_kstride + w_off), static_cast<short>(0),
+      static_cast<int>(s.OC * R * 4), 0x00020000);
   // this thread gathers pixel px0 + t of the tile
   const int64_t px = px0 + t;
   const bool px_ok = px < NPX;
-  int ih0 = 0, iw0 = 0;
-  const float* xp = x;
+  int ih0 = 0, iw0 = 0, vbase = 0;
   if (px_ok) {
     const int64_t m = px / OHW;
     const int64_t ohw = px - m * OHW;
@@ -1593,10 +1604,11 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
     const int ow = static_cast<int>(ohw - int64_t(oh) * s.OW);
     ih0 = oh * static_cast<int>(s.stride_h) - static_cast<int>(s.pad_h);
     iw0 = ow * static_cast<int>(s.stride_w) - static_cast<int>(s.pad_w);
-    xp = x + k * x_kstride + m * s.C * HW;
+    vbase = static_cast<int>(m * s.C * HW) + ih0 * static_cast<int>(s.W) + iw0;
   }
   const int H = static_cast<int>(s.H), W = static_cast<int>(s.W);
   const int KH = static_cast<int>(s.KH), KW = static_cast<int>(s.KW);
+  const int iHW = static_cast<int>(HW), iR = static_cast<int>(R);
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1606,25 +1618,29 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   constexpr int WPT = kTC_OC * RK / 256;  // weight elements per thread per stage
   float rw[WPT], rx[RK];
-  // wave-uniform walk of r = (c, kh, kw) through the stage
-  auto fetch = [&](int64_t r0) {
+  auto fetch = [&](int r0) {
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
       const int e = t + 256 * j;
-      const int64_t oc = oc0 + e / RK;
-      const int64_t r = r0 + e % RK;
-      rw[j] = (oc < s.OC && r < R) ? wk[oc * R + r] : 0.f;
+      const int oc = static_cast<int>(oc0) + e / RK;
+      const int r = r0 + e % RK;
+      const uint32_t off = (oc < s.OC && r < iR) ? static_cast<uint32_t>(oc * iR + r) * 4u : kOut;
+      rw[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            wres, static_cast<int>(off), 0, 0));
     }
-    int64_t c = r0 / (s.KH * s.KW);
-    int rr = static_cast<int>(r0 - c * s.KH * s.KW);
+    // wave-uniform walk of r = (c, kh, kw) through the stage
+    int c = r0 / (KH * KW);
+    const int rr = r0 - c * KH * KW;
     int kh = rr / KW;
     int kw = rr - kh * KW;
 #pragma unroll
     for (int i = 0; i < RK; ++i) {
-      const int ih = ih0 + kh, iw = iw0 + kw;
-      const bool ok = px_ok && (r0 + i < R) && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
-      rx[i] = ok ? xp[c * HW + ih * W + iw] : 0.f;
+      const bool ok = px_ok && (r0 + i < iR) &&
+                      static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(W);
+      const uint32_t off = ok ? static_cast<uint32_t>(vbase + c * iHW + kh * W + kw) * 4u : kOut;
+      rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            xres, static_cast<int>(off), 0, 0));
       if (++kw == KW) {
         kw = 0;
         if (++kh == KH) {
@@ -1635,7 +1651,7 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
     }
   };
   fetch(0);
-  for (int64_t r0 = 0; r0 < R; r0 += RK) {
+  for (int r0 = 0; r0 < iR; r0 += RK) {
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
       const int e = t + 256 * j;
@@ -1644,7 +1660,7 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
 #pragma unroll
     for (int i = 0; i < RK; ++i) sX[i][t] = rx[i];
     __syncthreads();
-    if (r0 + RK < R) fetch(r0 + RK);
+    if (r0 + RK < iR) fetch(r0 + RK);
     const int col = lane & 31;
     const int kk = lane >> 5;
 #pragma unroll
@@ -1683,6 +1699,8 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
   }
 }
 
+constexpr int kPoolCB = 16;  // channels per workgroup of the pool pass (register window)
+
 // ---------------------------------------------------------------------------
 // The memory-bound chain that follows a convolution in the reference's CNNs
 // (fedsim/models/simple_models.py:245-252, SimpleCNN2: relu -> F.pad(0,1,0,1)
@@ -1697,6 +1715,69 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
 // avg = s / size, d = pow(fl32(fl32(avg * alpha) + k), beta), y = x / d.
 // Max pool: -inf start, NaN sticks (max_pool2d's CUDA kernel).
 // ---------------------------------------------------------------------------
+// LRN of one element from its channel window, ATen's sequence
+// (torch/nn/functional.py local_response_norm): avg = s / size (exact as a
+// multiply when size is a power of two), d = (avg * alpha + k) ^ beta, v / d.
+// FAST: the power is exp2(beta * log2(b)) on the transcendental unit
+// (v_log_f32 / v_exp_f32), valid for a normal positive base b -- the LRN's
+// case, b >= k > 0 -- and within a few ulps of powf at a small fraction of its
+// instructions (the pass is VALU-bound on powf otherwise); lrn_fast_ok says
+// whether it applies.  !FAST: powf.
+__device__ __forceinline__ bool lrn_fast_ok(float b) {
+  return b >= 1.17549435e-38f && b < 3.0e38f;
+}
+
+template <int SIZE, bool FAST>
+__device__ __forceinline__ float lrn_value(float v, float sum, float size_f, float alpha,
+                                           float beta, float k, bool* fast_ok = nullptr) {
+  float avg;
+  if constexpr (SIZE > 0 && (SIZE & (SIZE - 1)) == 0)
+    avg = sum * (1.0f / SIZE);
+  else
+    avg = sum / size_f;
+  const float b = avg * alpha + k;
+  float d;
+  if constexpr (FAST) {
+    if (fast_ok && !lrn_fast_ok(b)) *fast_ok = false;
+    d = __builtin_amdgcn_exp2f(beta * __builtin_amdgcn_logf(b));
+  } else {
+    d = powf(b, beta);
+  }
+  return v / d;
+}
+
+// Phase 2 of both variants: max-pool the CB padded planes in LDS into y.
+__device__ __forceinline__ void pool_planes(const float* plane, int cbn, int Hp, int Wp,
+                                            const fedagg_pool_args& a, int OH, int OW,
+                                            float* __restrict__ yn) {
+  const int OHW = OH * OW;
+  const int HpWp = Hp * Wp;
+  const int kh = static_cast<int>(a.pool_kh), kw = static_cast<int>(a.pool_kw);
+  for (int e = threadIdx.x; e < cbn * OHW; e += 256) {
+    const int cc = e / OHW;
+    const int q = e - cc * OHW;
+    const int oh = q / OW;
+    const int ow = q - oh * OW;
+    const int hs = oh * static_cast<int>(a.pool_sh) - static_cast<int>(a.pool_ph);
+    const int ws = ow * static_cast<int>(a.pool_sw) - static_cast<int>(a.pool_pw);
+    const int he = min(hs + kh, Hp), we = min(ws + kw, Wp);
+    const int h0 = max(hs, 0), w0 = max(ws, 0);
+    const float* pl = plane + cc * HpWp;
+    float m = -__builtin_inff();
+    for (int h = h0; h < he; ++h)
+      for (int w = w0; w < we; ++w) {
+        const float v = pl[h * Wp + w];
+        if (v > m || __builtin_isnan(v)) m = v;
+      }
+    yn[e] = m;
+  }
+}
+
+// SIZE = the LRN window (0: no LRN) known at compile time: each thread loads
+// the whole channel window of its pixel for the block (CB + SIZE - 1 values,
+// all loads in flight at once) and normalises CB channels from registers.
+// SIZE < 0: any window, loaded per channel (the general fallback).
+template <int SIZE>
 __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict__ x,
                                                          fedagg_pool_args a, int64_t CB,
                                                          int64_t OH, int64_t OW,
@@ -1713,15 +1794,18 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
   const int HW = H * W;
   const int C = static_cast<int>(a.C);
   const float* xn = x + n * a.C * HW;
-  const int lo = static_cast<int>(a.lrn_size / 2);
   const float size_f = static_cast<float>(a.lrn_size);
-  for (int q = threadIdx.x; q < HpWp; q += 256) {
+  // the general path: every channel of the block for the pixel at plane
+  // position q, its window loaded per channel, powf (any LRN size; also the
+  // redo of a pixel whose base fell outside the fast power's range)
+  auto general = [&](int q) {
     const int ph = q / Wp;
     const int ih = ph - static_cast<int>(a.pad_top);
     const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
     const bool in = static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
                     static_cast<unsigned>(iw) < static_cast<unsigned>(W);
     const int off = ih * W + iw;
+    const int lo = static_cast<int>(a.lrn_size / 2);
     for (int cc = 0; cc < cbn; ++cc) {
       float v = 0.f;
       if (in) {
@@ -1731,39 +1815,59 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
           float sum = 0.f;
           for (int t = 0; t < a.lrn_size; ++t) {
             const int ch = c - lo + t;
-            const float u = static_cast<unsigned>(ch) < static_cast<unsigned>(C) ? xn[ch * HW + off] : 0.f;
+            const float u =
+                static_cast<unsigned>(ch) < static_cast<unsigned>(C) ? xn[ch * HW + off] : 0.f;
             sum = sum + u * u;
           }
-          const float avg = sum / size_f;
-          const float d = powf(avg * a.lrn_alpha + a.lrn_k, a.lrn_beta);
-          v = v / d;
+          v = lrn_value<-1, false>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
         }
       }
       plane[cc * HpWp + q] = v;
     }
+  };
+  if constexpr (SIZE >= 0) {
+    bool fast_ok = true;
+    for (int q = threadIdx.x; q < HpWp; q += 256) {
+      const int ph = q / Wp;
+      const int ih = ph - static_cast<int>(a.pad_top);
+      const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
+      const bool in = static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const int off = ih * W + iw;
+      constexpr int LO = SIZE / 2;
+      constexpr int NV = kPoolCB + (SIZE > 0 ? SIZE - 1 : 0);
+      float xr[NV];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int ch = static_cast<int>(c0) - LO + j;
+        xr[j] = (in && static_cast<unsigned>(ch) < static_cast<unsigned>(C) &&
+                 ch < static_cast<int>(c0) + cbn + (SIZE > 0 ? SIZE - 1 - LO : 0))
+                    ? xn[ch * HW + off] : 0.f;
+      }
+      bool ok = true;
+#pragma unroll
+      for (int cc = 0; cc < kPoolCB; ++cc) {
+        if (cc < cbn) {
+          float v = xr[cc + LO];
+          if constexpr (SIZE > 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int t = 0; t < SIZE; ++t) sum = sum + xr[cc + t] * xr[cc + t];
+            if (in) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k, &ok);
+          }
+          plane[cc * HpWp + q] = v;
+        }
+      }
+      fast_ok = fast_ok && ok;
+    }
+    if (!fast_ok)  // rare: recompute this thread's pixels with powf
+      for (int q = threadIdx.x; q < HpWp; q += 256) general(q);
+  } else {
+    for (int q = threadIdx.x; q < HpWp; q += 256) general(q);
   }
   __syncthreads();
-  const int OHW = static_cast<int>(OH * OW);
-  const int kh = static_cast<int>(a.pool_kh), kw = static_cast<int>(a.pool_kw);
-  float* yn = y + (n * a.C + c0) * OHW;
-  for (int q = threadIdx.x; q < OHW; q += 256) {
-    const int oh = q / static_cast<int>(OW);
-    const int ow = q - oh * static_cast<int>(OW);
-    const int hs = oh * static_cast<int>(a.pool_sh) - static_cast<int>(a.pool_ph);
-    const int ws = ow * static_cast<int>(a.pool_sw) - static_cast<int>(a.pool_pw);
-    const int he = min(hs + kh, Hp), we = min(ws + kw, Wp);
-    const int h0 = max(hs, 0), w0 = max(ws, 0);
-    for (int cc = 0; cc < cbn; ++cc) {
-      const float* pl = plane + cc * HpWp;
-      float m = -__builtin_inff();
-      for (int h = h0; h < he; ++h)
-        for (int w = w0; w < we; ++w) {
-          const float v = pl[h * Wp + w];
-          if (v > m || __builtin_isnan(v)) m = v;
-        }
-      yn[cc * OHW + q] = m;
-    }
-  }
+  pool_planes(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
+              y + (n * a.C + c0) * OH * OW);
 }
 
 }  // namespace
@@ -1963,28 +2067,35 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
       s.stride_w >= lim || s.pad_h >= lim || s.pad_w >= lim || s.OH >= lim || s.OW >= lim ||
       s.H * s.W >= (int64_t(1) << 31))
     return FEDAGG_EINVAL;
-  // every output window must start inside the padded input
-  if ((s.OH - 1) * s.stride_h - s.pad_h >= s.H || (s.OW - 1) * s.stride_w - s.pad_w >= s.W)
-    return FEDAGG_EINVAL;
   const int64_t R = s.C * s.KH * s.KW;
   if (K > 1 && (w_off + s.OC * R > params_kstride || (b_off >= 0 && b_off + s.OC > params_kstride)))
+    return FEDAGG_EINVAL;
+  // one teacher's input and weight matrix are addressed by 32-bit buffer offsets
+  if (s.M * s.C * s.H * s.W >= (int64_t(1) << 29) || s.OC * R >= (int64_t(1) << 29))
     return FEDAGG_EINVAL;
   if (K == 0 || s.M == 0) return 0;
   if (!x || !params || !y) return FEDAGG_EINVAL;
   const int64_t oc_tiles = (s.OC + kTC_OC - 1) / kTC_OC;
   const int64_t px_tiles = (s.M * s.OH * s.OW + kTC_PX - 1) / kTC_PX;
-  const int64_t tiles = K * oc_tiles * px_tiles;
-  if (tiles > (int64_t(1) << 31) - 1) return FEDAGG_EINVAL;
+  if (px_tiles > (int64_t(1) << 31) - 1 || oc_tiles > 65535) return FEDAGG_EINVAL;
   const int relu = (flags & FEDAGG_RELU) ? 1 : 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (fedagg_conv_stage(R) == 16)
-    hipLaunchKernelGGL(k_teacher_conv2d<16>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st,
-                       x, x_kstride, params, params_kstride, w_off, b_off, s, y, oc_tiles,
-                       px_tiles, relu);
-  else
-    hipLaunchKernelGGL(k_teacher_conv2d<32>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st,
-                       x, x_kstride, params, params_kstride, w_off, b_off, s, y, oc_tiles,
-                       px_tiles, relu);
+  for (int64_t k0 = 0; k0 < K; k0 += 65535) {  // grid z: at most 65535 teachers per launch
+    const int64_t kn = K - k0 < 65535 ? K - k0 : 65535;
+    const dim3 grid(static_cast<unsigned>(px_tiles), static_cast<unsigned>(oc_tiles),
+                    static_cast<unsigned>(kn));
+    const float* xk = x + k0 * x_kstride;
+    const float* pk = params + k0 * params_kstride;
+    float* yk = y + k0 * s.M * s.OC * s.OH * s.OW;
+    if (fedagg_conv_stage(R) == 16)
+      hipLaunchKernelGGL(k_teacher_conv2d<16>, grid, dim3(256), 0, st, xk, x_kstride, pk,
+                         params_kstride, w_off, b_off, s, yk, relu);
+    else
+      hipLaunchKernelGGL(k_teacher_conv2d<32>, grid, dim3(256), 0, st, xk, x_kstride, pk,
+                         params_kstride, w_off, b_off, s, yk, relu);
+    const int rc = static_cast<int>(hipGetLastError());
+    if (rc) return rc;
+  }
   return static_cast<int>(hipGetLastError());
 }
 
@@ -2008,11 +2119,13 @@ int fedagg_pool_output(const fedagg_pool_args* a, int64_t* OH, int64_t* OW, int6
   if (Hp + 2 * ph < kh || Wp + 2 * pw < kw) return FEDAGG_EINVAL;
   *OH = (Hp + 2 * ph - kh) / sh + 1;
   *OW = (Wp + 2 * pw - kw) / sw + 1;
-  // channels per workgroup: their padded planes fit 32 KiB of LDS, balanced over the blocks
+  // channels per workgroup: at most kPoolCB, their padded planes within 40 KiB
+  // of LDS (four workgroups per CU), balanced over the blocks
   const int64_t plane = Hp * Wp;
   if (plane > 16384) return FEDAGG_EINVAL;
-  int64_t cb = 8192 / plane;
+  int64_t cb = 10240 / plane;
   if (cb < 1) cb = 1;
+  if (cb > kPoolCB) cb = kPoolCB;
   if (cb > a->C) cb = a->C;
   const int64_t nblk = (a->C + cb - 1) / cb;
   *CB = (a->C + nblk - 1) / nblk;
@@ -2035,8 +2148,15 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
   if (blocks > (int64_t(1) << 31) - 1) return FEDAGG_EINVAL;
   const int64_t Hp = a.H + a.pad_top + a.pad_bottom, Wp = a.W + a.pad_left + a.pad_right;
   const size_t lds = static_cast<size_t>(CB * Hp * Wp) * sizeof(float);
-  hipLaunchKernelGGL(k_pad_lrn_maxpool, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
-                     static_cast<hipStream_t>(stream), x, a, CB, OH, OW, y);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(blocks));
+  switch (a.lrn_size) {
+    case 0: hipLaunchKernelGGL(k_pad_lrn_maxpool<0>, grid, dim3(256), lds, st, x, a, CB, OH, OW, y); break;
+    case 3: hipLaunchKernelGGL(k_pad_lrn_maxpool<3>, grid, dim3(256), lds, st, x, a, CB, OH, OW, y); break;
+    case 4: hipLaunchKernelGGL(k_pad_lrn_maxpool<4>, grid, dim3(256), lds, st, x, a, CB, OH, OW, y); break;
+    case 5: hipLaunchKernelGGL(k_pad_lrn_maxpool<5>, grid, dim3(256), lds, st, x, a, CB, OH, OW, y); break;
+    default: hipLaunchKernelGGL(k_pad_lrn_maxpool<-1>, grid, dim3(256), lds, st, x, a, CB, OH, OW, y);
+  }
   return static_cast<int>(hipGetLastError());
 }
 

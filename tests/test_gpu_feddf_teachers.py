@@ -253,7 +253,9 @@ POOL_CASES = [
     ((3, 32, 28, 28), (0, 0, 0, 0), None, (2, 2, 2, 2, 1, 1)),                       # SimpleCNN
     ((2, 5, 7, 9), (1, 2, 0, 3), (3, 0.01, 0.5, 2.0), None),                         # no pool
     ((2, 3, 6, 5), (0, 0, 0, 0), (5, 1.0, 1.25, 0.5), (2, 3, 1, 2, 1, 1)),           # C < size
-    ((1, 70, 30, 31), (2, 0, 1, 1), (4, 1e-4, 0.75, 1.0), (3, 2, 3, 2, 1, 0)),       # 2 channels / WG
+    ((1, 70, 30, 31), (2, 0, 1, 1), (4, 1e-4, 0.75, 1.0), (3, 2, 3, 2, 1, 0)),       # ragged blocks
+    ((2, 20, 9, 9), (1, 1, 1, 1), (7, 2e-3, 0.6, 1.5), (3, 3, 3, 3, 1, 1)),          # any-size LRN
+    ((1, 3, 120, 120), (0, 0, 0, 0), (3, 1e-3, 0.75, 1.0), (2, 2, 2, 2, 0, 0)),      # 1 channel / WG
 ]
 
 
@@ -277,7 +279,7 @@ def test_pad_lrn_maxpool_kernel(case):
         np.testing.assert_array_equal(got, exp)
     else:
         ulp = np.spacing(np.abs(exp).astype(np.float32))
-        assert float((np.abs(got - exp) / ulp).max()) <= 2.0
+        assert float((np.abs(got - exp) / ulp).max()) <= 8.0  # hardware exp2 / log2 power
     F = torch.nn.functional
     t, b, l, r = pads
     want = F.pad(x, (l, r, t, b))
@@ -286,7 +288,7 @@ def test_pad_lrn_maxpool_kernel(case):
     if pool is not None:
         kh, kw, sh, sw, ph, pw = pool
         want = F.max_pool2d(want, (kh, kw), (sh, sw), (ph, pw))
-    torch.testing.assert_close(y, want, rtol=3e-7, atol=0)
+    torch.testing.assert_close(y, want, rtol=1e-6, atol=0)
 
 
 def test_pad_lrn_maxpool_special_values():
