@@ -223,7 +223,7 @@ def test_conv_and_pool_host_side_shapes(lib):
     a = ops.pool_args((8, 64, 24, 24), (0, 1, 0, 1), None, (3, 3, 2, 2, 0, 0))
     assert lib.fedagg_pool_output(ctypes.byref(a), ctypes.byref(oh), ctypes.byref(ow),
                                   ctypes.byref(cb)) == 0
-    assert cb.value * 625 * 4 <= 32768 and cb.value >= 1
+    assert cb.value * 625 * 4 <= 40960 and cb.value >= 1  # padded planes within 40 KiB of LDS
     for bad in (ops.pool_args((1, 1, 200, 200)),                         # plane > 64 KiB
                 ops.pool_args((1, 1, 8, 8), pool=(2, 2, 2, 2, 2, 0)),    # padding > kernel / 2
                 ops.pool_args((1, 1, 2, 2), pool=(3, 3, 1, 1, 0, 0)),    # kernel > input
