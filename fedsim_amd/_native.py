@@ -36,6 +36,7 @@ FEDAGG_LDSW = 0x20000
 FEDAGG_MAP_SHIFT = 18
 FEDAGG_FAST = 0x200000
 FEDAGG_RELU = 0x400000
+FEDAGG_CONV_GATHER = 0x800000
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0
@@ -147,6 +148,7 @@ SIGNATURES = {
          ctypes.c_int, ctypes.c_void_p],
     ),
     "fedagg_conv_stage": (ctypes.c_int, [ctypes.c_int64]),
+    "fedagg_conv_order": (ctypes.c_int, [ctypes.POINTER(Conv2dShape), ctypes.c_int]),
     "fedagg_pool_output": (
         ctypes.c_int,
         [ctypes.POINTER(PoolArgs), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),

@@ -1699,6 +1699,243 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same convolution with the input tile resident in LDS (stride 1, square
+// KS x KS kernels: every Conv2d of the reference's CNNs, 5 x 5).  The gather
+// above spends ~20 address instructions per im2col element, more issue slots
+// than its MFMAs get; here a workgroup stages, per chunk of CC input
+// channels, the zero-padded planes of the (at most nslot) images its 256
+// output pixels fall in, [nslot][CC][Hp][Wp], plus the chunk's weights in
+// their own layout, [64 oc][CC * KS * KS] (odd row pitch: 32 rows hit 32
+// banks).  An MFMA operand is then ONE ds_read_b32 at a per-lane base + an
+// immediate offset: the k pair of v_mfma_f32_32x32x2_f32 is two adjacent
+// channels (kk = lane >> 5 is folded into the per-lane base), the tap (kh, kw)
+// and the channel pair are the immediate.  Chain order per output (restated
+// by oracle/fedagg_ref.c ref_teacher_conv2d_f32 with cc = CC): channel
+// chunks, then kh, then channel pairs, then kw, then the pair's two channels;
+// channels past C (C odd) are zero terms.  The chunk's planes and weights
+// are loaded into registers while the previous chunk's MFMAs run; the halo
+// of the planes is zeroed once and never written.  Offsets for the plane
+// staging are decoded once per thread (packed: global << 0 | LDS << 18).
+// ---------------------------------------------------------------------------
+constexpr int kTC_XPK_LDS = 14;  // LDS float index bits of a packed staging offset
+constexpr int kTC_XPK_GLB = 18;  // global float offset bits
+
+template <int KS, int CC, int XM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_lds(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
+    float* __restrict__ y, int relu) {
+  constexpr int TAPS = KS * KS;
+  constexpr int RC = TAPS * CC;  // reductions per chunk
+  constexpr int RW = RC + 1;     // sW row pitch (odd)
+  constexpr int WPT = (RC + 3) / 4;  // weight columns per thread per chunk
+  extern __shared__ float lds[];
+  float* sW = lds;
+  float* sX = lds + kTC_OC * RW;
+  // grid (pixel tiles, channel tiles, teachers): tile coordinates straight
+  // from the SGPRs, so the buffer descriptors below are provably uniform (one
+  // derived from a VALU division costs a waterfall loop per load)
+  const int64_t k = blockIdx.z;
+  const int oc0 = blockIdx.y * kTC_OC;
+  const int pxt = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int C = static_cast<int>(s.C), H = static_cast<int>(s.H), W = static_cast<int>(s.W);
+  const int OW = static_cast<int>(s.OW);
+  const int OHW = static_cast<int>(s.OH * s.OW);
+  const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = OW + KS - 1, HpWp = Hp * Wp;
+  const int HW = H * W;
+  const int NPX = static_cast<int>(s.M) * OHW;
+  const int R = C * TAPS;
+  const int OC = static_cast<int>(s.OC);
+  const int px0 = pxt * kTC_PX;
+  const int m_lo = px0 / OHW;  // first image of the tile (VGPR: offsets only)
+  const int pt = static_cast<int>(s.pad_h), pl = static_cast<int>(s.pad_w);
+  // the images of this tile (reads past the teacher's last image are 0) and
+  // the teacher's [OC][C][KS][KS] weights
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + k * x_kstride), static_cast<short>(0),
+      static_cast<int>(s.M * C * HW * 4), 0x00020000);
+  const uint32_t x_tile4 = static_cast<uint32_t>(m_lo * C * HW) * 4u;
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(params + k * params_kstride + w_off), static_cast<short>(0),
+      OC * R * 4, 0x00020000);
+  const int plane_n = nslot * HW;  // staged elements per channel of a chunk
+  const int xtot = CC * plane_n;
+  // plane staging: element e = t + 256 i of a chunk is (channel cl, slot,
+  // hw), cl slowest; packed: its global float offset from the tile's first
+  // image (channel c0 added per chunk as the scalar offset) and its LDS index
+  uint32_t xpk[XM];
+#pragma unroll
+  for (int i = 0; i < XM; ++i) {
+    const int e = t + 256 * i;
+    if (e < xtot) {
+      const int cl = e / plane_n;
+      const int rem = e - cl * plane_n;
+      const int slot = rem / HW;
+      const int hw = rem - slot * HW;
+      const int h = hw / W;
+      const int w = hw - h * W;
+      const uint32_t g = static_cast<uint32_t>(slot * C * HW + cl * HW + hw);
+      const uint32_t l = static_cast<uint32_t>(((slot * CC + cl) * Hp + h + pt) * Wp + w + pl);
+      xpk[i] = g | (l << kTC_XPK_GLB);
+    } else {
+      xpk[i] = 0xffffffffu;
+    }
+  }
+  for (int i = t; i < nslot * CC * HpWp; i += 256) sX[i] = 0.f;
+  __syncthreads();  // the halo zeroes land before any thread stages a plane
+  // weight staging: thread t owns output channel oc0 + t / 4 and the chunk
+  // columns j = t % 4 + 4 i (one VGPR base, immediate offsets); rows past OC
+  // read 0 through the descriptor's range
+  const int wq = t & 3;
+  const uint32_t wg4 = static_cast<uint32_t>((oc0 + (t >> 2)) * R + wq) * 4u;
+  const int wl = (t >> 2) * RW + wq;
+  float rw[WPT], rx[XM];
+  auto fetch = [&](int c0) {
+    const int soff_w = c0 * TAPS * 4;
+    const int soff_x = c0 * HW * 4;
+    if (C - c0 >= CC) {  // a full chunk (every chunk unless C is odd)
+#pragma unroll
+      for (int i = 0; i < WPT; ++i)
+        rw[i] = (wq + 4 * i < RC)
+                    ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    wres, static_cast<int>(wg4 + 16u * i), soff_w, 0))
+                    : 0.f;
+#pragma unroll
+      for (int i = 0; i < XM; ++i) {
+        const uint32_t g4 = (xpk[i] & ((1u << kTC_XPK_GLB) - 1u)) * 4u + x_tile4;
+        rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              xres, static_cast<int>(g4), soff_x, 0));
+      }
+    } else {  // the last chunk of an odd C: channels past C are zero terms
+      const int jlim = (C - c0) * TAPS;
+      const int xlim = (C - c0) * plane_n;
+#pragma unroll
+      for (int i = 0; i < WPT; ++i)
+        rw[i] = (wq + 4 * i < RC && wq + 4 * i < jlim)
+                    ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    wres, static_cast<int>(wg4 + 16u * i), soff_w, 0))
+                    : 0.f;
+#pragma unroll
+      for (int i = 0; i < XM; ++i) {
+        const uint32_t g4 = (xpk[i] & ((1u << kTC_XPK_GLB) - 1u)) * 4u + x_tile4;
+        rx[i] = (t + 256 * i < xlim)
+                    ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    xres, static_cast<int>(g4), soff_x, 0))
+                    : 0.f;
+      }
+    }
+  };
+  // operand bases: A = weights (oc = lane & 31 [+ 32], channel + kk), B =
+  // the staged planes at this lane's output pixel (channel + kk)
+  const int col = lane & 31;
+  const int kk = lane >> 5;
+  const int wa = col * RW + kk * TAPS;
+  int xb[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    int p = px0 + wave * 64 + b * 32 + col;
+    p = p < NPX ? p : NPX - 1;
+    const int m = p / OHW;
+    const int ohw = p - m * OHW;
+    const int oh = ohw / OW;
+    const int ow = ohw - oh * OW;
+    xb[b] = ((m - m_lo) * CC + kk) * HpWp + oh * Wp + ow;
+  }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  fetch(0);
+  for (int c0 = 0; c0 < C; c0 += CC) {
+#pragma unroll
+    for (int i = 0; i < WPT; ++i)
+      if (wq + 4 * i < RC) sW[wl + 4 * i] = rw[i];
+#pragma unroll
+    for (int i = 0; i < XM; ++i)
+      if (xpk[i] != 0xffffffffu) sX[xpk[i] >> kTC_XPK_GLB] = rx[i];
+    __syncthreads();
+    if (c0 + CC < C) fetch(c0 + CC);
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll
+      for (int cp = 0; cp < CC / 2; ++cp) {
+        const float* pb0 = sX + xb[0] + 2 * cp * HpWp + kh * Wp;
+        const float* pb1 = sX + xb[1] + 2 * cp * HpWp + kh * Wp;
+        const float* pa = sW + wa + 2 * cp * TAPS + kh * KS;
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const float a0 = pa[kw];
+          const float a1 = pa[32 * RW + kw];
+          const float b0 = pb0[kw];
+          const float b1 = pb1[kw];
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int p = px0 + wave * 64 + b * 32 + col;
+    if (p >= NPX) continue;
+    const int m = p / OHW;
+    float* yp = y + (k * s.M + m) * s.OC * OHW + (p - m * OHW);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
+        if (oc >= OC) continue;
+        float v = acc[a][b][e] + (bk ? bk[oc] : 0.f);
+        if (relu) v = v > 0.f ? v : 0.f;
+        yp[int64_t(oc) * OHW] = v;
+      }
+    }
+  }
+}
+
+// Launch plan of k_teacher_conv2d_lds for a shape, or false (the gather
+// kernel runs it).  cc: channels per chunk, xm: staging registers per
+// thread, nslot: images a 256-pixel tile can touch, lds: bytes.
+struct ConvLdsPlan {
+  int ks, cc, xm, nslot;
+  size_t lds;
+};
+
+bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
+  if (s.KH != s.KW || (s.KH != 5 && s.KH != 3) || s.stride_h != 1 || s.stride_w != 1) return false;
+  const int64_t ks = s.KH;
+  const int64_t Hp = s.OH + ks - 1, Wp = s.OW + ks - 1;
+  if (s.H + s.pad_h > Hp || s.W + s.pad_w > Wp) return false;  // input rows past the window
+  const int64_t OHW = s.OH * s.OW, HW = s.H * s.W;
+  if (s.M * OHW >= (int64_t(1) << 31)) return false;
+  int64_t nslot = (kTC_PX - 2) / OHW + 2;
+  if (nslot > s.M) nslot = s.M;
+  const int cc = s.C >= 4 ? 4 : 2;
+  const int64_t xtot = cc * nslot * HW;
+  const int xm = xtot <= 8 * 256 ? 8 : 16;
+  if (xtot > xm * 256) return false;
+  if (nslot * cc * Hp * Wp >= (int64_t(1) << kTC_XPK_LDS)) return false;
+  if (nslot * s.C * HW + cc * HW >= (int64_t(1) << kTC_XPK_GLB)) return false;
+  p->ks = static_cast<int>(ks);
+  p->cc = cc;
+  p->xm = xm;
+  p->nslot = static_cast<int>(nslot);
+  p->lds = static_cast<size_t>(kTC_OC * (cc * ks * ks + 1) + nslot * cc * Hp * Wp) * sizeof(float);
+  return p->lds <= 64 * 1024;
+}
+
 constexpr int kPoolCB = 16;  // channels per workgroup of the pool pass (register window)
 
 // ---------------------------------------------------------------------------
@@ -2051,13 +2288,19 @@ int fedagg_conv_stage(int64_t R) {
   return ((R + 15) / 16 * 16 < (R + 31) / 32 * 32) ? 16 : 32;
 }
 
+int fedagg_conv_order(const fedagg_conv2d_shape* shape, int flags) {
+  ConvLdsPlan plan;
+  if (!shape || (flags & FEDAGG_CONV_GATHER) || !conv_lds_plan(*shape, &plan)) return 0;
+  return plan.cc;
+}
+
 int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* params,
                               int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t K,
                               const fedagg_conv2d_shape* shape, float* y, int flags,
                               void* stream) {
   if (!shape || K < 0 || x_kstride < 0 || params_kstride < 0 || w_off < 0 || b_off < -1)
     return FEDAGG_EINVAL;
-  if (flags & ~FEDAGG_RELU) return FEDAGG_EINVAL;
+  if (flags & ~(FEDAGG_RELU | FEDAGG_CONV_GATHER)) return FEDAGG_EINVAL;
   const fedagg_conv2d_shape s = *shape;
   const int64_t lim = int64_t(1) << 15;
   if (s.M < 0 || s.C <= 0 || s.H <= 0 || s.W <= 0 || s.OC <= 0 || s.KH <= 0 || s.KW <= 0 ||
@@ -2080,6 +2323,37 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   if (px_tiles > (int64_t(1) << 31) - 1 || oc_tiles > 65535) return FEDAGG_EINVAL;
   const int relu = (flags & FEDAGG_RELU) ? 1 : 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  ConvLdsPlan plan;
+  if (!(flags & FEDAGG_CONV_GATHER) && conv_lds_plan(s, &plan)) {
+    for (int64_t k0 = 0; k0 < K; k0 += 65535) {
+      const int64_t kn = K - k0 < 65535 ? K - k0 : 65535;
+      const dim3 grid(static_cast<unsigned>(px_tiles), static_cast<unsigned>(oc_tiles),
+                      static_cast<unsigned>(kn));
+      const float* xk = x + k0 * x_kstride;
+      const float* pk = params + k0 * params_kstride;
+      float* yk = y + k0 * s.M * s.OC * s.OH * s.OW;
+#define FEDAGG_CONV_LDS(KS, CC, XM)                                                          \
+  hipLaunchKernelGGL((k_teacher_conv2d_lds<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
+                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
+      if (plan.ks == 5) {
+        if (plan.cc == 4) {
+          if (plan.xm == 8) FEDAGG_CONV_LDS(5, 4, 8); else FEDAGG_CONV_LDS(5, 4, 16);
+        } else {
+          if (plan.xm == 8) FEDAGG_CONV_LDS(5, 2, 8); else FEDAGG_CONV_LDS(5, 2, 16);
+        }
+      } else {
+        if (plan.cc == 4) {
+          if (plan.xm == 8) FEDAGG_CONV_LDS(3, 4, 8); else FEDAGG_CONV_LDS(3, 4, 16);
+        } else {
+          if (plan.xm == 8) FEDAGG_CONV_LDS(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
+        }
+      }
+#undef FEDAGG_CONV_LDS
+      const int rc = static_cast<int>(hipGetLastError());
+      if (rc) return rc;
+    }
+    return 0;
+  }
   for (int64_t k0 = 0; k0 < K; k0 += 65535) {  // grid z: at most 65535 teachers per launch
     const int64_t kn = K - k0 < 65535 ? K - k0 : 65535;
     const dim3 grid(static_cast<unsigned>(px_tiles), static_cast<unsigned>(oc_tiles),

@@ -405,15 +405,37 @@ def teacher_linear(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int, 
     return y
 
 
+def conv_shape(x_shape, out_channels: int, kernel_size, stride, padding) -> "_native.Conv2dShape":
+    """struct fedagg_conv2d_shape of a conv over x [..., M, C, H, W] with
+    ``padding`` = (top, bottom, left, right)."""
+    M, C, H, W = x_shape[-4:]
+    KH, KW = kernel_size
+    sh, sw = stride
+    pt, pb, pl, pr = padding
+    OH = (H + pt + pb - KH) // sh + 1
+    OW = (W + pl + pr - KW) // sw + 1
+    return _native.Conv2dShape(M, C, H, W, out_channels, KH, KW, sh, sw, pt, pl, OH, OW)
+
+
+def conv_order(x_shape, out_channels: int, kernel_size, stride, padding,
+               gather: bool = False) -> int:
+    """The fmaf chain order teacher_conv2d takes for this geometry
+    (fedagg_conv_order): 0 = (c, kh, kw), else the LDS kernel's channel chunk."""
+    s = conv_shape(x_shape, out_channels, kernel_size, stride, padding)
+    return int(_native.load().fedagg_conv_order(ctypes.byref(s),
+                                                _native.FEDAGG_CONV_GATHER if gather else 0))
+
+
 def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
                    out_channels: int, kernel_size, stride, padding, shared: bool,
-                   relu: bool = False) -> torch.Tensor:
+                   relu: bool = False, gather: bool = False) -> torch.Tensor:
     """One nn.Conv2d (groups 1, dilation 1, zero padding) of the K teachers
     whose flat parameter vectors are the rows of ``slab`` ([K, P]), as an
     implicit GEMM on the matrix cores (fedagg_teacher_conv2d_f32).  ``x``:
     [M, C, H, W] shared by every teacher (``shared``) or [K, M, C, H, W].
     ``padding`` = (top, bottom, left, right) zeros.  Returns
-    y [K, M, OC, OH, OW] (ReLU applied when ``relu``).  b_off = -1: no bias."""
+    y [K, M, OC, OH, OW] (ReLU applied when ``relu``).  b_off = -1: no bias.
+    ``gather``: the im2col-gather kernel even where the LDS one applies."""
     _require_hip_f32(x, "x")
     _require_hip_f32(slab, "slab")
     if slab.dim() != 2 or not slab.is_contiguous() or x.device != slab.device:
@@ -438,7 +460,8 @@ def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
     y = torch.empty((K, M, out_channels, OH, OW), dtype=torch.float32, device=x.device)
     rc = _native.load().fedagg_teacher_conv2d_f32(
         x.data_ptr(), 0 if shared else M * C * H * W, slab.data_ptr(), P, w_off, b_off, K,
-        ctypes.byref(shape), y.data_ptr(), _native.FEDAGG_RELU if relu else 0,
+        ctypes.byref(shape), y.data_ptr(),
+        (_native.FEDAGG_RELU if relu else 0) | (_native.FEDAGG_CONV_GATHER if gather else 0),
         _stream_ptr(x.device))
     check(rc, "fedagg_teacher_conv2d_f32")
     return y

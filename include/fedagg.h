@@ -103,6 +103,10 @@ extern "C" {
 /* fedagg_teacher_linear_f32: apply ReLU to the layer's output (a following
  * torch.relu / nn.ReLU fused into the layer) */
 #define FEDAGG_RELU     0x400000
+/* fedagg_teacher_conv2d_f32: take the im2col-gather kernel even where the
+ * LDS-resident one applies (A/B and its own tests; same results up to the
+ * chain order fedagg_conv_order reports) */
+#define FEDAGG_CONV_GATHER 0x800000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
@@ -200,9 +204,14 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
  * fits).  x_k = x + k*x_kstride ([M, C, H, W] contiguous; x_kstride = 0: one
  * input shared by all teachers); W_k = params + k*params_kstride + w_off
  * ([OC, C, KH, KW] row-major, the teacher's flat vector); b_off = -1: no
- * bias.  y is [K, M, OC, OH, OW] contiguous.  flags: FEDAGG_RELU.  Each
- * output is the exact f32 fmaf chain over r = (c, kh, kw) in order from
- * +0.0f, then one bias add: normwise, not bitwise, equal to a CPU conv.
+ * bias.  y is [K, M, OC, OH, OW] contiguous.  flags: FEDAGG_RELU,
+ * FEDAGG_CONV_GATHER.  Each output is an exact f32 fmaf chain from +0.0f,
+ * then one bias add: normwise, not bitwise, equal to a CPU conv.  The chain's
+ * order is what fedagg_conv_order reports for the shape:
+ *   0  (the im2col-gather kernel): r = (c, kh, kw) in order;
+ *   cc (the LDS-resident kernel: stride 1, KH = KW = 3 or 5): channel chunks
+ *      of cc, then kh, then channel pairs, then kw, then the pair's two
+ *      channels; channels past C are fmaf(0, 0, acc) terms.
  */
 typedef struct fedagg_conv2d_shape {
   int64_t M, C, H, W;          /* per-teacher input [M, C, H, W]            */
@@ -220,6 +229,10 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
 /* Reductions per LDS stage the conv kernel takes for R = C*KH*KW (16 or 32;
  * the exact chain is the same either way). Host-side, no device access. */
 int fedagg_conv_stage(int64_t R);
+
+/* Chain order of fedagg_teacher_conv2d_f32 for this shape and flags: 0 for
+ * the (c, kh, kw) order, else the channel chunk cc (see above). Host-side. */
+int fedagg_conv_order(const fedagg_conv2d_shape* shape, int flags);
 
 /*
  * The memory-bound chain after a convolution of the reference's CNNs

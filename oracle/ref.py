@@ -48,7 +48,7 @@ def lib():
         L.ref_teacher_linear_f32.argtypes = [vp, i64, vp, i64, i64, i64, i64, i64, i64, i64,
                                              vp, ci]
         L.ref_teacher_conv2d_f32.argtypes = [vp, i64, vp, i64, i64, i64, i64] + [i64] * 13 + [
-            vp, ci]
+            vp, ci, i64]
         L.ref_pad_lrn_maxpool_f32.argtypes = [vp] + [i64] * 9 + [f32] * 3 + [i64] * 6 + [vp]
         for fn in ("ref_reduce_f32", "ref_finalize_f32", "ref_fedavg_sgd_f32",
                    "ref_adabest_sgd_f32", "ref_feddyn_sgd_f32", "ref_server_step_f32",
@@ -195,10 +195,12 @@ def teacher_linear(x: np.ndarray, slab: np.ndarray, w_off: int, b_off: int, in_f
 
 
 def teacher_conv2d(x: np.ndarray, slab: np.ndarray, w_off: int, b_off: int, out_channels: int,
-                   kernel_size, stride, padding, shared: bool, relu: bool = False) -> np.ndarray:
+                   kernel_size, stride, padding, shared: bool, relu: bool = False,
+                   cc: int = 0) -> np.ndarray:
     """C oracle of fedagg_teacher_conv2d_f32 (the fmaf chain over
-    (c, kh, kw) in order; see fedagg_ref.c).  padding = (top, bottom, left,
-    right); returns [K, M, OC, OH, OW]."""
+    (c, kh, kw) in order, or, cc > 0, the LDS-resident kernel's chunked order
+    that fedagg_conv_order reports; see fedagg_ref.c).  padding = (top,
+    bottom, left, right); returns [K, M, OC, OH, OW]."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     slab = np.ascontiguousarray(slab, dtype=np.float32)
     K, P = slab.shape
@@ -211,7 +213,7 @@ def teacher_conv2d(x: np.ndarray, slab: np.ndarray, w_off: int, b_off: int, out_
     y = np.empty((K, M, out_channels, OH, OW), dtype=np.float32)
     lib().ref_teacher_conv2d_f32(_p(x), 0 if shared else M * C * H * W, _p(slab), P, w_off, b_off,
                                  K, M, C, H, W, out_channels, KH, KW, sh, sw, pt, pl, OH, OW,
-                                 _p(y), int(relu))
+                                 _p(y), int(relu), int(cc))
     return y
 
 

@@ -44,7 +44,8 @@ def test_header_declares_the_abi():
         "fedagg_reduce_rows_f32",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_pack_segments_f32",
         "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_teacher_conv2d_f32",
-        "fedagg_conv_stage", "fedagg_pool_output", "fedagg_pad_lrn_maxpool_f32",
+        "fedagg_conv_stage", "fedagg_conv_order", "fedagg_pool_output",
+        "fedagg_pad_lrn_maxpool_f32",
         "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
@@ -211,6 +212,17 @@ def test_conv_and_pool_host_side_shapes(lib):
 
     assert [lib.fedagg_conv_stage(r) for r in (0, 1, 16, 17, 32, 75, 96, 1600)] == \
         [0, 16, 16, 32, 32, 16, 32, 32]
+    # which chain order (kernel) a conv takes: SimpleCNN2's two 5x5 "same"
+    # convs go to the LDS-resident kernel (chunks of 2 / 4 channels); a
+    # strided conv, a 7x7 kernel, or the gather flag keep the (c, kh, kw) chain
+    same = (2, 2, 2, 2)
+    assert ops.conv_order((64, 3, 24, 24), 64, (5, 5), (1, 1), same) == 2
+    assert ops.conv_order((64, 64, 12, 12), 64, (5, 5), (1, 1), same) == 4
+    assert ops.conv_order((64, 32, 14, 14), 64, (5, 5), (1, 1), (1, 1, 1, 1)) == 4  # SimpleCNN
+    assert ops.conv_order((64, 64, 12, 12), 64, (5, 5), (1, 1), same, gather=True) == 0
+    assert ops.conv_order((64, 64, 12, 12), 64, (5, 5), (2, 2), same) == 0
+    assert ops.conv_order((64, 64, 12, 12), 64, (7, 7), (1, 1), (3, 3, 3, 3)) == 0
+    assert ops.conv_order((64, 4, 40, 40), 8, (5, 5), (1, 1), same) == 0  # tile past the LDS plan
     # SimpleCNN2 (simple_models.py:245-252): 24x24 -> pad 25x25 -> pool 3/2 -> 12x12; 12 -> 13 -> 6
     a = ops.pool_args((64, 64, 24, 24), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0))
     assert ops.pool_output(a) == (12, 12)

@@ -161,6 +161,13 @@ CONV_CASES = [
     (4, 7, 11, 10, 100, (3, 3), (2, 2), (1, 1, 1, 1)),   # stride 2, two channel tiles
     (5, 2, 6, 6, 3, (1, 1), (1, 1), (0, 0, 0, 0)),       # 1x1
     (1, 33, 5, 5, 65, (5, 5), (1, 3), (0, 0, 4, 0)),     # R = 825, ragged everything
+    # the LDS-resident kernel (stride 1, 3x3 / 5x5): chunk tails, image slots
+    (9, 5, 12, 12, 64, (5, 5), (1, 1), (2, 2, 2, 2)),    # C = 5: a one-channel last chunk
+    (3, 2, 10, 7, 130, (3, 3), (1, 1), (1, 1, 1, 1)),    # chunks of 2, three channel tiles
+    (40, 6, 4, 4, 17, (3, 3), (1, 1), (0, 2, 2, 0)),     # 16-pixel images: 17 per tile
+    (2, 8, 9, 11, 64, (5, 5), (1, 1), (0, 4, 3, 1)),     # asymmetric padding
+    (1, 4, 20, 20, 8, (5, 5), (1, 1), (0, 0, 0, 0)),     # valid conv, one image
+    (2, 4, 40, 40, 8, (5, 5), (1, 1), (2, 2, 2, 2)),     # tile too big for LDS: gather kernel
 ]
 
 
@@ -185,14 +192,17 @@ def test_teacher_conv2d_kernel_is_the_fmaf_chain(case, shared):
     slab = torch.randn(K, P, device=DEV, generator=g)
     x = torch.randn((M, C, H, W) if shared else (K, M, C, H, W), device=DEV, generator=g)
     x.view(-1)[:: 97] = -0.0
-    for bias, relu in ((True, False), (False, True), (True, True)):
-        b_off = w_off + OC * R if bias else -1
-        y = ops.teacher_conv2d(x, slab, w_off, b_off, OC, kern, stride, pads, shared=shared,
-                               relu=relu)
-        exp = ref.teacher_conv2d(x.cpu().numpy(), slab.cpu().numpy(), w_off, b_off, OC, kern,
-                                 stride, pads, shared, relu)
-        assert y.shape == exp.shape
-        np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp))
+    for gather in (False, True):
+        cc = ops.conv_order(x.shape, OC, kern, stride, pads, gather=gather)
+        for bias, relu in ((True, False), (False, True), (True, True)):
+            b_off = w_off + OC * R if bias else -1
+            y = ops.teacher_conv2d(x, slab, w_off, b_off, OC, kern, stride, pads, shared=shared,
+                                   relu=relu, gather=gather)
+            exp = ref.teacher_conv2d(x.cpu().numpy(), slab.cpu().numpy(), w_off, b_off, OC,
+                                     kern, stride, pads, shared, relu, cc=cc)
+            assert y.shape == exp.shape
+            np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp),
+                                          err_msg=f"gather={gather} cc={cc}")
     # and the chain is a convolution: fp64 within gamma_R
     F = torch.nn.functional
     Wt = slab[:, w_off:w_off + OC * R].view(K, OC, C, *kern).double()
@@ -217,13 +227,17 @@ def test_teacher_conv2d_random_shapes_bitwise():
     from oracle import ref
 
     rng = np.random.default_rng(355)
-    for _ in range(30):
+    lds_cases = 0
+    for it in range(40):
         K = int(rng.integers(1, 4))
         M = int(rng.integers(1, 4))
         C = int(rng.integers(1, 20))
         H, W = int(rng.integers(1, 14)), int(rng.integers(1, 14))
         kh, kw = int(rng.integers(1, min(H, 5) + 1)), int(rng.integers(1, min(W, 5) + 1))
         sh, sw = int(rng.integers(1, 3)), int(rng.integers(1, 3))
+        if it % 3 == 0 and min(H, W) >= 3:  # a geometry the LDS-resident kernel takes
+            kh = kw = 5 if min(H, W) >= 5 and it % 2 else 3
+            sh = sw = 1
         pads = tuple(int(v) for v in rng.integers(0, 3, 4))
         OC = int(rng.integers(1, 80))
         R = C * kh * kw
@@ -236,14 +250,17 @@ def test_teacher_conv2d_random_shapes_bitwise():
         x.reshape(-1)[:: max(1, x.size // 5)] = np.float32(-0.0)
         relu = bool(rng.integers(0, 2))
         b_off = w_off + OC * R if bias else -1
+        cc = ops.conv_order(x.shape, OC, (kh, kw), (sh, sw), pads)
+        lds_cases += cc > 0
         y = ops.teacher_conv2d(torch.from_numpy(x).to(DEV), torch.from_numpy(slab).to(DEV),
                                w_off, b_off, OC, (kh, kw), (sh, sw), pads, shared=shared,
                                relu=relu)
         exp = ref.teacher_conv2d(x, slab, w_off, b_off, OC, (kh, kw), (sh, sw), pads, shared,
-                                 relu)
+                                 relu, cc=cc)
         np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp),
                                       err_msg=f"K={K} M={M} C={C} HxW={H}x{W} k={kh}x{kw} "
-                                              f"s={sh}x{sw} pads={pads} OC={OC}")
+                                              f"s={sh}x{sw} pads={pads} OC={OC} cc={cc}")
+    assert lds_cases >= 5  # the LDS-resident kernel is among them
 
 
 # (shape, pads, lrn, pool)
