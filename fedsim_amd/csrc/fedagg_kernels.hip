@@ -2107,6 +2107,113 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
               y + (n * a.C + c0) * OH * OW);
 }
 
+// The same pass for planes of at most 256 * NQ positions (every pool of the
+// reference's CNNs): grid (channel blocks, images) so the image's buffer
+// descriptor is uniform, and ALL of a thread's NQ x (CB + SIZE - 1) channel
+// window loads are issued before the first LRN, one latency per workgroup
+// instead of one per 256 positions.  Per load: one VGPR offset for the
+// position (out of range: past the descriptor, reads 0), the channel as the
+// scalar offset.  Same arithmetic as k_pad_lrn_maxpool<SIZE>.
+template <int SIZE, int NQ>
+__global__ __launch_bounds__(256) void k_pad_lrn_maxpool_q(const float* __restrict__ x,
+                                                           fedagg_pool_args a, int64_t CB,
+                                                           int64_t OH, int64_t OW,
+                                                           int64_t n_base,
+                                                           float* __restrict__ y) {
+  extern __shared__ float plane[];
+  const int64_t n = n_base + blockIdx.y;
+  const int c0 = static_cast<int>(blockIdx.x * CB);
+  const int cbn = static_cast<int>(a.C - c0 < CB ? a.C - c0 : CB);
+  const int H = static_cast<int>(a.H), W = static_cast<int>(a.W);
+  const int Hp = H + static_cast<int>(a.pad_top + a.pad_bottom);
+  const int Wp = W + static_cast<int>(a.pad_left + a.pad_right);
+  const int HpWp = Hp * Wp;
+  const int HW = H * W;
+  const int C = static_cast<int>(a.C);
+  const float* xn = x + n * a.C * HW;
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xn), static_cast<short>(0), static_cast<int>(a.C * HW * 4), 0x00020000);
+  constexpr uint32_t kOut = 0x80000000u;
+  constexpr int LO = SIZE > 0 ? SIZE / 2 : 0;
+  constexpr int NV = kPoolCB + (SIZE > 0 ? SIZE - 1 : 0);
+  // the block's channels and their LRN halo: c0 - LO + j, j < NV, real
+  // channels only (wave-uniform)
+  const int jhi = cbn + (SIZE > 0 ? SIZE - 1 : 0);
+  float xr[NQ][NV];
+  uint32_t voff[NQ];
+  bool in[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    const int ph = q / Wp;
+    const int ih = ph - static_cast<int>(a.pad_top);
+    const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
+    in[i] = q < HpWp && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+            static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+    voff[i] = in[i] ? static_cast<uint32_t>(ih * W + iw) * 4u : kOut;
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int ch = c0 - LO + j;
+    const bool ok = ch >= 0 && ch < C && j < jhi;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i)
+      xr[i][j] = ok ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    xres, static_cast<int>(voff[i]), ch * HW * 4, 0))
+                    : 0.f;
+  }
+  const float size_f = static_cast<float>(a.lrn_size);
+  bool fast_ok = true;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    if (q < HpWp) {
+      bool ok = true;
+#pragma unroll
+      for (int cc = 0; cc < kPoolCB; ++cc) {
+        if (cc < cbn) {
+          float v = xr[i][cc + LO];
+          if constexpr (SIZE > 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int t = 0; t < SIZE; ++t) sum = sum + xr[i][cc + t] * xr[i][cc + t];
+            if (in[i])
+              v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k, &ok);
+          }
+          plane[cc * HpWp + q] = v;
+        }
+      }
+      fast_ok = fast_ok && ok;
+    }
+  }
+  if (!fast_ok) {  // rare: this thread's positions again with powf
+    const int lo = static_cast<int>(a.lrn_size / 2);
+    for (int q = threadIdx.x; q < HpWp; q += 256) {
+      const int ph = q / Wp;
+      const int ih = ph - static_cast<int>(a.pad_top);
+      const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
+      if (static_cast<unsigned>(ih) >= static_cast<unsigned>(H) ||
+          static_cast<unsigned>(iw) >= static_cast<unsigned>(W))
+        continue;
+      const int off = ih * W + iw;
+      for (int cc = 0; cc < cbn; ++cc) {
+        const int c = c0 + cc;
+        float sum = 0.f;
+        for (int t = 0; t < a.lrn_size; ++t) {
+          const int ch = c - lo + t;
+          const float u = static_cast<unsigned>(ch) < static_cast<unsigned>(C) ? xn[ch * HW + off] : 0.f;
+          sum = sum + u * u;
+        }
+        plane[cc * HpWp + q] =
+            lrn_value<-1, false>(xn[c * HW + off], sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
+      }
+    }
+  }
+  __syncthreads();
+  pool_planes(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
+              y + (n * a.C + c0) * OH * OW);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2423,6 +2530,34 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
   const int64_t Hp = a.H + a.pad_top + a.pad_bottom, Wp = a.W + a.pad_left + a.pad_right;
   const size_t lds = static_cast<size_t>(CB * Hp * Wp) * sizeof(float);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t nq = (Hp * Wp + 255) / 256;
+  if (nq <= 4 && (a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5))) {
+    const int64_t nblk = (a.C + CB - 1) / CB;
+    for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {  // grid y: at most 65535 images per launch
+      const dim3 g(static_cast<unsigned>(nblk),
+                   static_cast<unsigned>(a.N - n0 < 65535 ? a.N - n0 : 65535));
+#define FEDAGG_POOL_Q(SZ, Q)                                                                   \
+  hipLaunchKernelGGL((k_pad_lrn_maxpool_q<SZ, Q>), g, dim3(256), lds, st, x, a, CB, OH, OW, n0, y)
+#define FEDAGG_POOL_NQ(SZ)                              \
+  switch (nq) {                                         \
+    case 1: FEDAGG_POOL_Q(SZ, 1); break;                \
+    case 2: FEDAGG_POOL_Q(SZ, 2); break;                \
+    case 3: FEDAGG_POOL_Q(SZ, 3); break;                \
+    default: FEDAGG_POOL_Q(SZ, 4);                      \
+  }
+      switch (a.lrn_size) {
+        case 0: FEDAGG_POOL_NQ(0); break;
+        case 3: FEDAGG_POOL_NQ(3); break;
+        case 4: FEDAGG_POOL_NQ(4); break;
+        default: FEDAGG_POOL_NQ(5);
+      }
+#undef FEDAGG_POOL_NQ
+#undef FEDAGG_POOL_Q
+      const int rc = static_cast<int>(hipGetLastError());
+      if (rc) return rc;
+    }
+    return 0;
+  }
   const dim3 grid(static_cast<unsigned>(blocks));
   switch (a.lrn_size) {
     case 0: hipLaunchKernelGGL(k_pad_lrn_maxpool<0>, grid, dim3(256), lds, st, x, a, CB, OH, OW, y); break;
