@@ -1956,17 +1956,21 @@ constexpr int kPoolCB = 16;  // channels per workgroup of the pool pass (registe
 // (torch/nn/functional.py local_response_norm): avg = s / size (exact as a
 // multiply when size is a power of two), d = (avg * alpha + k) ^ beta, v / d.
 // FAST: the power is exp2(beta * log2(b)) on the transcendental unit
-// (v_log_f32 / v_exp_f32), valid for a normal positive base b -- the LRN's
-// case, b >= k > 0 -- and within a few ulps of powf at a small fraction of its
-// instructions (the pass is VALU-bound on powf otherwise); lrn_fast_ok says
-// whether it applies.  !FAST: powf.
+// (v_log_f32 / v_exp_f32) for a normal positive base b -- the LRN's case,
+// b >= k > 0 -- within a few ulps of powf at a small fraction of its
+// instructions (the pass is VALU-bound on powf otherwise); any other base
+// (lrn_fast_ok false), and every element when !FAST, takes powf.
 __device__ __forceinline__ bool lrn_fast_ok(float b) {
   return b >= 1.17549435e-38f && b < 3.0e38f;
 }
 
+// the rare powf of a fast LRN, out of line: the unrolled channel loops would
+// otherwise carry one inlined powf each
+__device__ __noinline__ float lrn_powf(float b, float beta) { return powf(b, beta); }
+
 template <int SIZE, bool FAST>
 __device__ __forceinline__ float lrn_value(float v, float sum, float size_f, float alpha,
-                                           float beta, float k, bool* fast_ok = nullptr) {
+                                           float beta, float k) {
   float avg;
   if constexpr (SIZE > 0 && (SIZE & (SIZE - 1)) == 0)
     avg = sum * (1.0f / SIZE);
@@ -1974,12 +1978,10 @@ __device__ __forceinline__ float lrn_value(float v, float sum, float size_f, flo
     avg = sum / size_f;
   const float b = avg * alpha + k;
   float d;
-  if constexpr (FAST) {
-    if (fast_ok && !lrn_fast_ok(b)) *fast_ok = false;
-    d = __builtin_amdgcn_exp2f(beta * __builtin_amdgcn_logf(b));
-  } else {
+  if constexpr (FAST)
+    d = lrn_fast_ok(b) ? __builtin_amdgcn_exp2f(beta * __builtin_amdgcn_logf(b)) : lrn_powf(b, beta);
+  else
     d = powf(b, beta);
-  }
   return v / d;
 }
 
@@ -2033,8 +2035,7 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
   const float* xn = x + n * a.C * HW;
   const float size_f = static_cast<float>(a.lrn_size);
   // the general path: every channel of the block for the pixel at plane
-  // position q, its window loaded per channel, powf (any LRN size; also the
-  // redo of a pixel whose base fell outside the fast power's range)
+  // position q, its window loaded per channel, powf (any LRN size)
   auto general = [&](int q) {
     const int ph = q / Wp;
     const int ih = ph - static_cast<int>(a.pad_top);
@@ -2063,7 +2064,6 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
     }
   };
   if constexpr (SIZE >= 0) {
-    bool fast_ok = true;
     for (int q = threadIdx.x; q < HpWp; q += 256) {
       const int ph = q / Wp;
       const int ih = ph - static_cast<int>(a.pad_top);
@@ -2081,7 +2081,6 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
                  ch < static_cast<int>(c0) + cbn + (SIZE > 0 ? SIZE - 1 - LO : 0))
                     ? xn[ch * HW + off] : 0.f;
       }
-      bool ok = true;
 #pragma unroll
       for (int cc = 0; cc < kPoolCB; ++cc) {
         if (cc < cbn) {
@@ -2090,15 +2089,12 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool(const float* __restrict
             float sum = 0.f;
 #pragma unroll
             for (int t = 0; t < SIZE; ++t) sum = sum + xr[cc + t] * xr[cc + t];
-            if (in) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k, &ok);
+            if (in) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
           }
           plane[cc * HpWp + q] = v;
         }
       }
-      fast_ok = fast_ok && ok;
     }
-    if (!fast_ok)  // rare: recompute this thread's pixels with powf
-      for (int q = threadIdx.x; q < HpWp; q += 256) general(q);
   } else {
     for (int q = threadIdx.x; q < HpWp; q += 256) general(q);
   }
@@ -2163,12 +2159,10 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_q(const float* __restri
                     : 0.f;
   }
   const float size_f = static_cast<float>(a.lrn_size);
-  bool fast_ok = true;
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
     const int q = threadIdx.x + 256 * i;
     if (q < HpWp) {
-      bool ok = true;
 #pragma unroll
       for (int cc = 0; cc < kPoolCB; ++cc) {
         if (cc < cbn) {
@@ -2177,35 +2171,10 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_q(const float* __restri
             float sum = 0.f;
 #pragma unroll
             for (int t = 0; t < SIZE; ++t) sum = sum + xr[i][cc + t] * xr[i][cc + t];
-            if (in[i])
-              v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k, &ok);
+            if (in[i]) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
           }
           plane[cc * HpWp + q] = v;
         }
-      }
-      fast_ok = fast_ok && ok;
-    }
-  }
-  if (!fast_ok) {  // rare: this thread's positions again with powf
-    const int lo = static_cast<int>(a.lrn_size / 2);
-    for (int q = threadIdx.x; q < HpWp; q += 256) {
-      const int ph = q / Wp;
-      const int ih = ph - static_cast<int>(a.pad_top);
-      const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
-      if (static_cast<unsigned>(ih) >= static_cast<unsigned>(H) ||
-          static_cast<unsigned>(iw) >= static_cast<unsigned>(W))
-        continue;
-      const int off = ih * W + iw;
-      for (int cc = 0; cc < cbn; ++cc) {
-        const int c = c0 + cc;
-        float sum = 0.f;
-        for (int t = 0; t < a.lrn_size; ++t) {
-          const int ch = c - lo + t;
-          const float u = static_cast<unsigned>(ch) < static_cast<unsigned>(C) ? xn[ch * HW + off] : 0.f;
-          sum = sum + u * u;
-        }
-        plane[cc * HpWp + q] =
-            lrn_value<-1, false>(xn[c * HW + off], sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
       }
     }
   }
