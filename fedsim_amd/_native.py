@@ -37,6 +37,7 @@ FEDAGG_MAP_SHIFT = 18
 FEDAGG_FAST = 0x200000
 FEDAGG_RELU = 0x400000
 FEDAGG_CONV_GATHER = 0x800000
+FEDAGG_POOL_PLANES = 0x1000000
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0
@@ -89,6 +90,7 @@ class PoolArgs(ctypes.Structure):
                  ("N", "C", "H", "W", "pad_top", "pad_bottom", "pad_left", "pad_right",
                   "lrn_size")]
                 + [(n, ctypes.c_float) for n in ("lrn_alpha", "lrn_beta", "lrn_k")]
+                + [("flags", ctypes.c_int32)]
                 + [(n, ctypes.c_int64) for n in
                    ("pool_kh", "pool_kw", "pool_sh", "pool_sw", "pool_ph", "pool_pw")])
 

@@ -1905,6 +1905,152 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
 }
 
+// ---------------------------------------------------------------------------
+// The LDS-resident convolution for inputs of few channels (CI = 1 or 3: the
+// first conv of the reference's CNNs, grayscale and RGB).  The chunked
+// kernel above pairs two CHANNELS per MFMA k step, so CI = 3 runs as 4
+// channels and CI = 1 as 2: a third / half of its matrix-core work is zero
+// terms.  Here every channel is staged at once and the k pairs run over the
+// flattened reduction index r = (c, kh, kw): ceil(CI*KS*KS / 2) steps, one
+// zero term at most (a zero weight times a zero register: exact).  The k
+// pair of a lane differs in its plane offset, chosen per step from two
+// compile-time constants.  Chain order = the natural (c, kh, kw) order
+// (fedagg_conv_order 0, oracle ref_teacher_conv2d_f32 with cc = 0): a
+// trailing +0 term leaves a chain that never holds -0 unchanged.
+// ---------------------------------------------------------------------------
+template <int KS, int CI, int XM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_flat(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
+    float* __restrict__ y, int relu) {
+  constexpr int TAPS = KS * KS;
+  constexpr int R = CI * TAPS;
+  constexpr int RP = (R + 1) / 2;    // k steps
+  constexpr int RW = 2 * RP + 1;     // sW row pitch (odd)
+  constexpr int WPT = (2 * RP + 3) / 4;
+  extern __shared__ float lds[];
+  float* sW = lds;
+  float* sX = lds + kTC_OC * RW;
+  const int64_t k = blockIdx.z;
+  const int oc0 = blockIdx.y * kTC_OC;
+  const int pxt = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int H = static_cast<int>(s.H), W = static_cast<int>(s.W);
+  const int OW = static_cast<int>(s.OW);
+  const int OHW = static_cast<int>(s.OH * s.OW);
+  const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = OW + KS - 1, HpWp = Hp * Wp;
+  const int HW = H * W;
+  const int NPX = static_cast<int>(s.M) * OHW;
+  const int OC = static_cast<int>(s.OC);
+  const int px0 = pxt * kTC_PX;
+  const int m_lo = px0 / OHW;
+  const int pt = static_cast<int>(s.pad_h), pl = static_cast<int>(s.pad_w);
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + k * x_kstride), static_cast<short>(0),
+      static_cast<int>(s.M * CI * HW * 4), 0x00020000);
+  const uint32_t x_tile4 = static_cast<uint32_t>(m_lo * CI * HW) * 4u;
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(params + k * params_kstride + w_off), static_cast<short>(0),
+      OC * R * 4, 0x00020000);
+  // stage every channel of the tile's images: element e = t + 256 i is
+  // (slot, channel, hw) in the input's own order, i.e. global offset e
+  const int xtot = nslot * CI * HW;
+  for (int i = t; i < nslot * CI * HpWp; i += 256) sX[i] = 0.f;
+  float rx[XM];
+#pragma unroll
+  for (int i = 0; i < XM; ++i) {
+    const int e = t + 256 * i;
+    rx[i] = e < xtot ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 xres, static_cast<int>(e * 4u + x_tile4), 0, 0))
+                     : 0.f;
+  }
+  // weights: thread t owns output channel oc0 + t / 4, columns t % 4 + 4 i
+  // (columns past R, and rows past OC, are zero)
+  const int wq = t & 3;
+  const uint32_t wg4 = static_cast<uint32_t>((oc0 + (t >> 2)) * R + wq) * 4u;
+  const int wl = (t >> 2) * RW + wq;
+  float rw[WPT];
+#pragma unroll
+  for (int i = 0; i < WPT; ++i)
+    rw[i] = (wq + 4 * i < R) ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     wres, static_cast<int>(wg4 + 16u * i), 0, 0))
+                             : 0.f;
+  __syncthreads();  // halo zeroes before the planes land
+#pragma unroll
+  for (int i = 0; i < XM; ++i) {
+    const int e = t + 256 * i;
+    if (e < xtot) {
+      const int sc = e / HW;  // slot * CI + channel
+      const int hw = e - sc * HW;
+      const int h = hw / W;
+      const int w = hw - h * W;
+      sX[(sc * Hp + h + pt) * Wp + w + pl] = rx[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < WPT; ++i)
+    if (wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
+  __syncthreads();
+  const int col = lane & 31;
+  const int kk = lane >> 5;
+  const float* pa = sW + col * RW + kk;
+  int xb[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    int p = px0 + wave * 64 + b * 32 + col;
+    p = p < NPX ? p : NPX - 1;
+    const int m = p / OHW;
+    const int ohw = p - m * OHW;
+    const int oh = ohw / OW;
+    const int ow = ohw - oh * OW;
+    xb[b] = (m - m_lo) * CI * HpWp + oh * Wp + ow;
+  }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+#pragma unroll
+  for (int st = 0; st < RP; ++st) {
+    const int r0 = 2 * st, r1 = 2 * st + 1;
+    const int o0 = (r0 / TAPS) * HpWp + ((r0 % TAPS) / KS) * Wp + r0 % KS;
+    const int o1 = r1 < R ? (r1 / TAPS) * HpWp + ((r1 % TAPS) / KS) * Wp + r1 % KS : 0;
+    const int ob = kk ? o1 : o0;
+    const float a0 = pa[2 * st];
+    const float a1 = pa[32 * RW + 2 * st];
+    float b0 = sX[xb[0] + ob];
+    float b1 = sX[xb[1] + ob];
+    if (r1 >= R && kk) b0 = b1 = 0.f;  // the zero term of an odd R
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+  }
+  const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int p = px0 + wave * 64 + b * 32 + col;
+    if (p >= NPX) continue;
+    const int m = p / OHW;
+    float* yp = y + (k * s.M + m) * s.OC * OHW + (p - m * OHW);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
+        if (oc >= OC) continue;
+        float v = acc[a][b][e] + (bk ? bk[oc] : 0.f);
+        if (relu) v = v > 0.f ? v : 0.f;
+        yp[int64_t(oc) * OHW] = v;
+      }
+    }
+  }
+}
+
 // Launch plan of k_teacher_conv2d_lds for a shape, or false (the gather
 // kernel runs it).  cc: channels per chunk, xm: staging registers per
 // thread, nslot: images a 256-pixel tile can touch, lds: bytes.
@@ -1922,6 +2068,18 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
   if (s.M * OHW >= (int64_t(1) << 31)) return false;
   int64_t nslot = (kTC_PX - 2) / OHW + 2;
   if (nslot > s.M) nslot = s.M;
+  if (s.C == 1 || s.C == 3) {  // every channel staged at once (k_teacher_conv2d_flat)
+    const int64_t xall = s.C * nslot * HW;
+    if (xall <= 16 * 256) {
+      const int64_t rw = (s.C * ks * ks + 1) / 2 * 2 + 1;
+      p->ks = static_cast<int>(ks);
+      p->cc = 0;
+      p->xm = xall <= 8 * 256 ? 8 : 16;
+      p->nslot = static_cast<int>(nslot);
+      p->lds = static_cast<size_t>(kTC_OC * rw + nslot * s.C * Hp * Wp) * sizeof(float);
+      if (p->lds <= 64 * 1024) return true;
+    }
+  }
   const int cc = s.C >= 4 ? 4 : 2;
   const int64_t xtot = cc * nslot * HW;
   const int xm = xtot <= 8 * 256 ? 8 : 16;
@@ -1937,6 +2095,17 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
 }
 
 constexpr int kPoolCB = 16;  // channels per workgroup of the pool pass (register window)
+
+// Channels per LDS block of the sliding-window pool pass for this chain
+// (k_pad_lrn_maxpool_slide, planes of <= 1024 positions, LRN size 0 / 3 /
+// 4 / 5; <= 24 KiB of LDS), or 0 when the per-block kernels run it (or the
+// caller asks for them with FEDAGG_POOL_PLANES).
+int pool_slide_cb(const fedagg_pool_args& a, int64_t plane) {
+  if (a.flags & FEDAGG_POOL_PLANES) return 0;
+  if (!(a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5))) return 0;
+  const int64_t nq = (plane + 255) / 256;
+  return nq == 1 ? 16 : nq <= 3 ? 8 : nq == 4 ? 4 : 0;
+}
 
 // ---------------------------------------------------------------------------
 // The memory-bound chain that follows a convolution in the reference's CNNs
@@ -2183,6 +2352,108 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_q(const float* __restri
               y + (n * a.C + c0) * OH * OW);
 }
 
+// The same pass with the LRN channel window SLIDING in registers (planes of
+// at most 256 * NQ positions).  A workgroup owns one image and a group of
+// channels [g0, g1), walked in blocks of CB: each position's window
+// (channels c - LO .. c + LEAD) lives in SW registers and advances one
+// channel at a time, so every input element is read from HBM once (the
+// per-block kernel above re-reads SIZE - 1 halo channels per block, across
+// XCDs, and gets four workgroups per CU from 40 KiB planes; here the planes
+// of a block take <= 20 KiB).  Software pipelined: the lead channels of
+// block b + 1 are loaded while block b is pooled out of LDS.  Same
+// arithmetic, element for element, as k_pad_lrn_maxpool_q<SIZE, NQ>.
+template <int SIZE, int NQ, int CB>
+__global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __restrict__ x,
+                                                               fedagg_pool_args a, int64_t CG,
+                                                               int64_t OH, int64_t OW,
+                                                               int64_t n_base,
+                                                               float* __restrict__ y) {
+  extern __shared__ float plane[];
+  constexpr int LO = SIZE > 0 ? SIZE / 2 : 0;
+  constexpr int SW = SIZE > 0 ? SIZE : 1;  // window registers per position
+  constexpr int LEAD = SW - 1 - LO;         // channels the window reaches past c
+  const int64_t n = n_base + blockIdx.y;
+  const int C = static_cast<int>(a.C);
+  const int g0 = static_cast<int>(blockIdx.x * CG);
+  const int g1 = static_cast<int>(a.C - g0 < CG ? a.C : g0 + CG);
+  const int H = static_cast<int>(a.H), W = static_cast<int>(a.W);
+  const int Hp = H + static_cast<int>(a.pad_top + a.pad_bottom);
+  const int Wp = W + static_cast<int>(a.pad_left + a.pad_right);
+  const int HpWp = Hp * Wp;
+  const int HW = H * W;
+  const int OHW = static_cast<int>(OH * OW);
+  const float* xn = x + n * a.C * HW;
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xn), static_cast<short>(0), static_cast<int>(a.C * HW * 4), 0x00020000);
+  constexpr uint32_t kOut = 0x80000000u;
+  uint32_t voff[NQ];
+  bool in[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    const int ph = q / Wp;
+    const int ih = ph - static_cast<int>(a.pad_top);
+    const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
+    in[i] = q < HpWp && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+            static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+    voff[i] = in[i] ? static_cast<uint32_t>(ih * W + iw) * 4u : kOut;
+  }
+  // channel ch of every position of this thread (0 outside [0, C): the
+  // LRN's zero channels; padded positions read past the descriptor: 0)
+  auto load = [&](float (&dst)[NQ], int ch) {
+    const bool ok = ch >= 0 && ch < C;  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < NQ; ++i)
+      dst[i] = ok ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  xres, static_cast<int>(voff[i]), ch * HW * 4, 0))
+                  : 0.f;
+  };
+  float win[SW][NQ];  // win[t] = channel c - LO + t of the current channel c
+#pragma unroll
+  for (int t = 0; t + 1 < SW; ++t) load(win[t + 1], g0 - LO + t);  // shifted in before use
+  float raw[CB][NQ];  // the lead channels c + LEAD of the block in flight
+#pragma unroll
+  for (int j = 0; j < CB; ++j) load(raw[j], g0 + LEAD + j);
+  const float size_f = static_cast<float>(a.lrn_size);
+  for (int c0 = g0; c0 < g1; c0 += CB) {
+    const int cbn = g1 - c0 < CB ? g1 - c0 : CB;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      if (j < cbn) {
+#pragma unroll
+        for (int t = 0; t + 1 < SW; ++t)
+#pragma unroll
+          for (int i = 0; i < NQ; ++i) win[t][i] = win[t + 1][i];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) win[SW - 1][i] = raw[j][i];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+          const int q = threadIdx.x + 256 * i;
+          if (q < HpWp) {
+            float v = win[LO][i];
+            if constexpr (SIZE > 0) {
+              float sum = 0.f;
+#pragma unroll
+              for (int t = 0; t < SIZE; ++t) sum = sum + win[t][i] * win[t][i];
+              if (in[i]) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
+            }
+            plane[j * HpWp + q] = v;
+          }
+        }
+      }
+    }
+    // the next block's lead channels fly while this block is pooled
+    if (c0 + CB < g1) {
+#pragma unroll
+      for (int j = 0; j < CB; ++j) load(raw[j], c0 + CB + LEAD + j);
+    }
+    __syncthreads();
+    pool_planes(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
+                y + (n * a.C + c0) * OHW);
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2411,7 +2682,24 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
 #define FEDAGG_CONV_LDS(KS, CC, XM)                                                          \
   hipLaunchKernelGGL((k_teacher_conv2d_lds<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
-      if (plan.ks == 5) {
+#define FEDAGG_CONV_FLAT(KS, CI, XM)                                                          \
+  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM>), grid, dim3(256), plan.lds, st, xk, \
+                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
+      if (plan.cc == 0) {
+        if (plan.ks == 5) {
+          if (s.C == 3) {
+            if (plan.xm == 8) FEDAGG_CONV_FLAT(5, 3, 8); else FEDAGG_CONV_FLAT(5, 3, 16);
+          } else {
+            if (plan.xm == 8) FEDAGG_CONV_FLAT(5, 1, 8); else FEDAGG_CONV_FLAT(5, 1, 16);
+          }
+        } else {
+          if (s.C == 3) {
+            if (plan.xm == 8) FEDAGG_CONV_FLAT(3, 3, 8); else FEDAGG_CONV_FLAT(3, 3, 16);
+          } else {
+            if (plan.xm == 8) FEDAGG_CONV_FLAT(3, 1, 8); else FEDAGG_CONV_FLAT(3, 1, 16);
+          }
+        }
+      } else if (plan.ks == 5) {
         if (plan.cc == 4) {
           if (plan.xm == 8) FEDAGG_CONV_LDS(5, 4, 8); else FEDAGG_CONV_LDS(5, 4, 16);
         } else {
@@ -2424,6 +2712,7 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
           if (plan.xm == 8) FEDAGG_CONV_LDS(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
         }
       }
+#undef FEDAGG_CONV_FLAT
 #undef FEDAGG_CONV_LDS
       const int rc = static_cast<int>(hipGetLastError());
       if (rc) return rc;
@@ -2469,10 +2758,15 @@ int fedagg_pool_output(const fedagg_pool_args* a, int64_t* OH, int64_t* OW, int6
   if (Hp + 2 * ph < kh || Wp + 2 * pw < kw) return FEDAGG_EINVAL;
   *OH = (Hp + 2 * ph - kh) / sh + 1;
   *OW = (Wp + 2 * pw - kw) / sw + 1;
-  // channels per workgroup: at most kPoolCB, their padded planes within 40 KiB
-  // of LDS (four workgroups per CU), balanced over the blocks
   const int64_t plane = Hp * Wp;
   if (plane > 16384) return FEDAGG_EINVAL;
+  const int slide = pool_slide_cb(*a, plane);
+  if (slide > 0) {  // sliding-window pass: channels per LDS block
+    *CB = slide < a->C ? slide : a->C;
+    return 0;
+  }
+  // channels per workgroup: at most kPoolCB, their padded planes within 40 KiB
+  // of LDS (four workgroups per CU), balanced over the blocks
   int64_t cb = 10240 / plane;
   if (cb < 1) cb = 1;
   if (cb > kPoolCB) cb = kPoolCB;
@@ -2500,6 +2794,43 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
   const size_t lds = static_cast<size_t>(CB * Hp * Wp) * sizeof(float);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nq = (Hp * Wp + 255) / 256;
+  if (pool_slide_cb(a, Hp * Wp) > 0) {
+    // channel groups: the whole C per image unless that leaves fewer than
+    // 2048 workgroups; each group a multiple of the LDS block
+    const int64_t cbs = pool_slide_cb(a, Hp * Wp);
+    const int64_t nb = (a.C + cbs - 1) / cbs;
+    int64_t G = (2048 + a.N - 1) / a.N;
+    if (G > nb) G = nb;
+    if (G < 1) G = 1;
+    const int64_t CG = ((nb + G - 1) / G) * cbs;
+    G = (a.C + CG - 1) / CG;
+    const size_t slds = static_cast<size_t>(cbs * Hp * Wp) * sizeof(float);
+    for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {
+      const dim3 g(static_cast<unsigned>(G),
+                   static_cast<unsigned>(a.N - n0 < 65535 ? a.N - n0 : 65535));
+#define FEDAGG_POOL_S(SZ, Q, B)                                                                 \
+  hipLaunchKernelGGL((k_pad_lrn_maxpool_slide<SZ, Q, B>), g, dim3(256), slds, st, x, a, CG, OH, \
+                     OW, n0, y)
+#define FEDAGG_POOL_SQ(SZ)                        \
+  switch (nq) {                                   \
+    case 1: FEDAGG_POOL_S(SZ, 1, 16); break;      \
+    case 2: FEDAGG_POOL_S(SZ, 2, 8); break;       \
+    case 3: FEDAGG_POOL_S(SZ, 3, 8); break;       \
+    default: FEDAGG_POOL_S(SZ, 4, 4);             \
+  }
+      switch (a.lrn_size) {
+        case 0: FEDAGG_POOL_SQ(0); break;
+        case 3: FEDAGG_POOL_SQ(3); break;
+        case 4: FEDAGG_POOL_SQ(4); break;
+        default: FEDAGG_POOL_SQ(5);
+      }
+#undef FEDAGG_POOL_SQ
+#undef FEDAGG_POOL_S
+      const int rc = static_cast<int>(hipGetLastError());
+      if (rc) return rc;
+    }
+    return 0;
+  }
   if (nq <= 4 && (a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5))) {
     const int64_t nblk = (a.C + CB - 1) / CB;
     for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {  // grid y: at most 65535 images per launch

@@ -467,17 +467,25 @@ def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
     return y
 
 
-def pool_args(shape, pads=(0, 0, 0, 0), lrn=None, pool=None) -> "_native.PoolArgs":
+def pool_args(shape, pads=(0, 0, 0, 0), lrn=None, pool=None,
+              planes: bool = False) -> "_native.PoolArgs":
     """struct fedagg_pool_args for an input of ``shape`` (..., C, H, W):
     ``pads`` (top, bottom, left, right) zeros, ``lrn`` (size, alpha, beta, k)
-    or None, ``pool`` (kh, kw, sh, sw, ph, pw) or None."""
+    or None, ``pool`` (kh, kw, sh, sw, ph, pw) or None.  ``planes``: take the
+    per-block kernels instead of the sliding channel window
+    (FEDAGG_POOL_PLANES; same bits, A/B and tests)."""
     C, H, W = shape[-3:]
     N = 1
     for d in shape[:-3]:
         N *= int(d)
     size, alpha, beta, k = lrn if lrn is not None else (0, 0.0, 0.0, 0.0)
     pk = pool if pool is not None else (0, 0, 0, 0, 0, 0)
-    return _native.PoolArgs(N, C, H, W, *pads, size, alpha, beta, k, *pk)
+    top, bottom, left, right = pads
+    return _native.PoolArgs(
+        N=N, C=C, H=H, W=W, pad_top=top, pad_bottom=bottom, pad_left=left, pad_right=right,
+        lrn_size=size, lrn_alpha=alpha, lrn_beta=beta, lrn_k=k,
+        flags=_native.FEDAGG_POOL_PLANES if planes else 0,
+        pool_kh=pk[0], pool_kw=pk[1], pool_sh=pk[2], pool_sw=pk[3], pool_ph=pk[4], pool_pw=pk[5])
 
 
 def pool_output(args) -> tuple:
@@ -491,14 +499,15 @@ def pool_output(args) -> tuple:
     return oh.value, ow.value
 
 
-def pad_lrn_maxpool(x: torch.Tensor, pads=(0, 0, 0, 0), lrn=None, pool=None) -> torch.Tensor:
+def pad_lrn_maxpool(x: torch.Tensor, pads=(0, 0, 0, 0), lrn=None, pool=None,
+                    planes: bool = False) -> torch.Tensor:
     """F.pad (zeros) -> F.local_response_norm -> F.max_pool2d over the last
     three dimensions (C, H, W) of ``x`` in one pass
     (fedagg_pad_lrn_maxpool_f32); leading dimensions are images."""
     _require_hip_f32(x, "x")
     if not x.is_contiguous() or x.dim() < 3:
         raise ValueError("x must be a contiguous (..., C, H, W) tensor")
-    args = pool_args(x.shape, pads, lrn, pool)
+    args = pool_args(x.shape, pads, lrn, pool, planes=planes)
     OH, OW = pool_output(args)
     y = torch.empty((*x.shape[:-2], OH, OW), dtype=torch.float32, device=x.device)
     rc = _native.load().fedagg_pad_lrn_maxpool_f32(x.data_ptr(), ctypes.byref(args), y.data_ptr(),

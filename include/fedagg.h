@@ -208,7 +208,9 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
  * FEDAGG_CONV_GATHER.  Each output is an exact f32 fmaf chain from +0.0f,
  * then one bias add: normwise, not bitwise, equal to a CPU conv.  The chain's
  * order is what fedagg_conv_order reports for the shape:
- *   0  (the im2col-gather kernel): r = (c, kh, kw) in order;
+ *   0  (the im2col-gather kernel, and the LDS-resident kernel for C = 1 or 3
+ *      with every channel staged at once): r = (c, kh, kw) in order, an odd
+ *      count closed by one fmaf(0, 0, acc) term;
  *   cc (the LDS-resident kernel: stride 1, KH = KW = 3 or 5): channel chunks
  *      of cc, then kh, then channel pairs, then kw, then the pair's two
  *      channels; channels past C are fmaf(0, 0, acc) terms.
@@ -249,13 +251,18 @@ int fedagg_conv_order(const fedagg_conv2d_shape* shape, int flags);
  *      floor mode, NaN propagates).  pool_kh = 0: no pooling.
  * Zero padding and LRN commute (LRN(0) = 0), so pad -> LRN and LRN -> pad
  * are both this call.  y is [N, C, OH, OW] contiguous; fedagg_pool_output
- * gives OH / OW (and the channels per workgroup).
+ * gives OH / OW (and the channels per workgroup / LDS block).
+ * flags: 0, or FEDAGG_POOL_PLANES to take the per-block kernels (each
+ * workgroup re-reads its block's LRN halo) instead of the sliding channel
+ * window for planes of <= 1024 positions; the results are the same bits.
  */
+#define FEDAGG_POOL_PLANES 0x1000000
 typedef struct fedagg_pool_args {
   int64_t N, C, H, W;
   int64_t pad_top, pad_bottom, pad_left, pad_right;
   int64_t lrn_size;
   float lrn_alpha, lrn_beta, lrn_k;
+  int32_t flags;
   int64_t pool_kh, pool_kw, pool_sh, pool_sw, pool_ph, pool_pw;
 } fedagg_pool_args;
 

@@ -212,11 +212,15 @@ def test_conv_and_pool_host_side_shapes(lib):
 
     assert [lib.fedagg_conv_stage(r) for r in (0, 1, 16, 17, 32, 75, 96, 1600)] == \
         [0, 16, 16, 32, 32, 16, 32, 32]
-    # which chain order (kernel) a conv takes: SimpleCNN2's two 5x5 "same"
-    # convs go to the LDS-resident kernel (chunks of 2 / 4 channels); a
-    # strided conv, a 7x7 kernel, or the gather flag keep the (c, kh, kw) chain
+    # which chain order (kernel) a conv takes: SimpleCNN2's conv2 goes to the
+    # LDS-resident kernel in chunks of 4 channels; its 3-channel conv1 (and
+    # any 1- or 3-channel 3x3 / 5x5 stride-1 conv) to the LDS-resident kernel
+    # with every channel staged, which keeps the (c, kh, kw) chain, as do a
+    # strided conv, a 7x7 kernel and the gather flag
     same = (2, 2, 2, 2)
-    assert ops.conv_order((64, 3, 24, 24), 64, (5, 5), (1, 1), same) == 2
+    assert ops.conv_order((64, 3, 24, 24), 64, (5, 5), (1, 1), same) == 0
+    assert ops.conv_order((64, 1, 28, 28), 32, (5, 5), (1, 1), same) == 0
+    assert ops.conv_order((64, 2, 24, 24), 64, (5, 5), (1, 1), same) == 2
     assert ops.conv_order((64, 64, 12, 12), 64, (5, 5), (1, 1), same) == 4
     assert ops.conv_order((64, 32, 14, 14), 64, (5, 5), (1, 1), (1, 1, 1, 1)) == 4  # SimpleCNN
     assert ops.conv_order((64, 64, 12, 12), 64, (5, 5), (1, 1), same, gather=True) == 0

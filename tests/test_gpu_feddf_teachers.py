@@ -168,6 +168,11 @@ CONV_CASES = [
     (2, 8, 9, 11, 64, (5, 5), (1, 1), (0, 4, 3, 1)),     # asymmetric padding
     (1, 4, 20, 20, 8, (5, 5), (1, 1), (0, 0, 0, 0)),     # valid conv, one image
     (2, 4, 40, 40, 8, (5, 5), (1, 1), (2, 2, 2, 2)),     # tile too big for LDS: gather kernel
+    # every channel staged (C = 1 / 3): flattened (c, kh, kw) pairs, odd R tails
+    (5, 3, 9, 9, 70, (3, 3), (1, 1), (1, 1, 1, 1)),      # R = 27, five image slots, 2 oc tiles
+    (2, 1, 30, 30, 16, (3, 3), (1, 1), (0, 0, 0, 0)),    # R = 9, valid conv
+    (3, 3, 16, 16, 64, (5, 5), (1, 1), (0, 4, 1, 3)),    # asymmetric padding
+    (1, 3, 30, 30, 33, (5, 5), (1, 1), (2, 2, 2, 2)),    # one image, 16 staging registers
 ]
 
 
@@ -306,6 +311,49 @@ def test_pad_lrn_maxpool_kernel(case):
         kh, kw, sh, sw, ph, pw = pool
         want = F.max_pool2d(want, (kh, kw), (sh, sw), (ph, pw))
     torch.testing.assert_close(y, want, rtol=1e-6, atol=0)
+    # the sliding channel window and the per-block kernels: the same bits
+    from conftest import bits
+
+    y_planes = ops.pad_lrn_maxpool(x, pads, lrn, pool, planes=True)
+    np.testing.assert_array_equal(bits(got), bits(y_planes.cpu().numpy()))
+
+
+# sliding-window pass: every plane size class (1..4 x 256 positions), LRN
+# sizes 0 / 3 / 4 / 5, ragged last blocks, channel groups at few images
+# (group boundaries inside the LRN window), C below the block
+SLIDE_CASES = [
+    ((1, 64, 24, 24), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0)),
+    ((7, 37, 12, 12), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0)),
+    ((3, 19, 20, 20), (1, 1, 1, 1), (3, 0.01, 0.5, 2.0), (2, 2, 2, 2, 0, 0)),
+    ((2, 45, 27, 27), (0, 1, 2, 0), (5, 1e-3, 0.75, 1.0), (3, 3, 2, 2, 1, 1)),
+    ((5, 11, 31, 32), (0, 0, 0, 1), (4, 2e-3, 0.6, 1.5), (2, 3, 2, 1, 1, 0)),
+    ((600, 9, 10, 10), (0, 0, 0, 0), None, (2, 2, 2, 2, 0, 0)),
+    ((2, 2, 16, 16), (1, 0, 0, 1), (5, 1.0, 1.25, 0.5), None),
+]
+
+
+@pytest.mark.parametrize("case", SLIDE_CASES)
+def test_pad_lrn_maxpool_slide_vs_planes(case):
+    """The sliding channel window (default for planes <= 1024 positions)
+    against the per-block kernels, bit for bit, and against the C oracle."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    shape, pads, lrn, pool = case
+    g = torch.Generator(device=DEV).manual_seed(7 * sum(shape))
+    x = torch.randn(*shape, device=DEV, generator=g) * 2
+    x.view(-1)[:: 53] = 0.0
+    y = ops.pad_lrn_maxpool(x, pads, lrn, pool)
+    y_planes = ops.pad_lrn_maxpool(x, pads, lrn, pool, planes=True)
+    np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(y_planes.cpu().numpy()))
+    exp = ref.pad_lrn_maxpool(x.cpu().numpy(), pads, lrn, pool)
+    got = y.cpu().numpy()
+    if lrn is None:
+        np.testing.assert_array_equal(got, exp)
+    else:
+        ulp = np.spacing(np.abs(exp).astype(np.float32))
+        assert float((np.abs(got - exp) / ulp).max()) <= 8.0
 
 
 def test_pad_lrn_maxpool_special_values():

@@ -1,7 +1,8 @@
 """FedDF teacher layers of SimpleCNN2 (fedsim/models/simple_models.py:245-252)
 at K stacked teachers, B = 64 samples, timed per launch with HIP events:
 conv1 (3 -> 64, 5x5, 24x24), the pad / LRN / max-pool pass after it, conv2
-(64 -> 64, 5x5, 12x12) and the pass after that.  Several libfedagg BUILD
+(64 -> 64, 5x5, 12x12) and the pass after that (sliding channel window, and
+FEDAGG_POOL_PLANES: the per-block kernels, "_planes").  Several libfedagg BUILD
 variants can be given; each is its own ctypes handle, run interleaved in one
 process, and every output is compared bitwise with the first library's.
 The convolutions run both ways: the default kernel choice ("lds" for these
@@ -65,8 +66,8 @@ def main():
         ops.check(rc, "conv")
         return y
 
-    def pad_pool(lib, x):
-        args = ops.pool_args(x.shape, (0, 1, 0, 1), lrn, pool)
+    def pad_pool(lib, x, planes=False):
+        args = ops.pool_args(x.shape, (0, 1, 0, 1), lrn, pool, planes=planes)
         oh, ow = ops.pool_output(args)
         y = torch.empty(*x.shape[:-2], oh, ow, device=dev)
         ops.check(lib.fedagg_pad_lrn_maxpool_f32(x.data_ptr(), ctypes.byref(args), y.data_ptr(),
@@ -88,8 +89,14 @@ def main():
         "conv2_gather": (lambda lib: conv(lib, p1, False, 64, 12, 12, c2w, c2b, True),
                          2.0 * K * M * 64 * 144 * 1600, 4.0 * 2 * K * M * 64 * 144),
         "pool2": (lambda lib: pad_pool(lib, c2), 0.0, 4.0 * K * M * 64 * (144 + 36)),
+        "pool1_planes": (lambda lib: pad_pool(lib, c1, True), 0.0, 4.0 * K * M * 64 * (576 + 144)),
+        "pool2_planes": (lambda lib: pad_pool(lib, c2, True), 0.0, 4.0 * K * M * 64 * (144 + 36)),
     }
     ref = {name: fn(libs[0]) for name, (fn, _, _) in layers.items()}
+    for name in ("pool1", "pool2"):  # sliding window vs per-block kernels: same bits
+        same = torch.equal(ref[name].view(torch.int32), ref[name + "_planes"].view(torch.int32))
+        print(json.dumps({"check": f"{name} slide vs planes", "bitwise": same}), flush=True)
+        assert same
     for name in ("conv1", "conv2"):  # the two chain orders agree normwise
         u, v = ref[name].double(), ref[name + "_gather"].double()
         rel = ((u - v).norm() / v.norm()).item()
