@@ -1918,8 +1918,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // (fedagg_conv_order 0, oracle ref_teacher_conv2d_f32 with cc = 0): a
 // trailing +0 term leaves a chain that never holds -0 unchanged.
 // ---------------------------------------------------------------------------
+#ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds;
+#define FEDAGG_FLAT_WPE 4  // 4: SimpleCNN2 conv1 2.26 ms vs 2.52 ms with 3, profiles/r02x3)
+#endif
 template <int KS, int CI, int XM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_flat(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
     float* __restrict__ y, int relu) {
@@ -2030,22 +2033,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
   }
+  // epilogue: each bias value loaded once for both pixel groups
   const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
+  float* yp[2];
+  bool pin[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int p = px0 + wave * 64 + b * 32 + col;
-    if (p >= NPX) continue;
-    const int m = p / OHW;
-    float* yp = y + (k * s.M + m) * s.OC * OHW + (p - m * OHW);
+    pin[b] = p < NPX;
+    const int pc = pin[b] ? p : 0;
+    const int m = pc / OHW;
+    yp[b] = y + (k * s.M + m) * s.OC * OHW + (pc - m * OHW);
+  }
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
+  for (int a = 0; a < 2; ++a) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
-        if (oc >= OC) continue;
-        float v = acc[a][b][e] + (bk ? bk[oc] : 0.f);
+    for (int e = 0; e < 16; ++e) {
+      const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
+      if (oc >= OC) continue;
+      const float bias = bk ? bk[oc] : 0.f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (!pin[b]) continue;
+        float v = acc[a][b][e] + bias;
         if (relu) v = v > 0.f ? v : 0.f;
-        yp[int64_t(oc) * OHW] = v;
+        yp[b][int64_t(oc) * OHW] = v;
       }
     }
   }
@@ -2178,6 +2190,67 @@ __device__ __forceinline__ void pool_planes(const float* plane, int cbn, int Hp,
         if (v > m || __builtin_isnan(v)) m = v;
       }
     yn[e] = m;
+  }
+}
+
+// pool_planes without a division per output: a thread's outputs e = t +
+// 256 i advance their (channel, oh, ow) by the mixed-radix digits of 256;
+// an unpadded 3 x 3 window (SimpleCNN2's pools) is read unrolled with no
+// bounds.  The same selection as pool_planes: scan order h then w, a later
+// element replaces the running max when greater or NaN.
+__device__ __forceinline__ void pool_planes_step(const float* plane, int cbn, int Hp, int Wp,
+                                                 const fedagg_pool_args& a, int OH, int OW,
+                                                 float* __restrict__ yn) {
+  const int OHW = OH * OW;
+  const int HpWp = Hp * Wp;
+  const int total = cbn * OHW;
+  const int sh = static_cast<int>(a.pool_sh), sw = static_cast<int>(a.pool_sw);
+  int e = threadIdx.x;
+  int cc = e / OHW;
+  int oh = (e - cc * OHW) / OW;
+  int ow = e - cc * OHW - oh * OW;
+  const int dcc = 256 / OHW;
+  const int doh = (256 - dcc * OHW) / OW;
+  const int dow = 256 - dcc * OHW - doh * OW;
+  if (a.pool_kh == 3 && a.pool_kw == 3 && a.pool_ph == 0 && a.pool_pw == 0) {
+    for (; e < total; e += 256) {
+      const float* p = plane + cc * HpWp + oh * sh * Wp + ow * sw;
+      float m = -__builtin_inff();
+#pragma unroll
+      for (int h = 0; h < 3; ++h)
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+          const float v = p[h * Wp + w];
+          if (v > m || __builtin_isnan(v)) m = v;
+        }
+      yn[e] = m;
+      ow += dow;
+      oh += doh;
+      if (ow >= OW) { ow -= OW; ++oh; }
+      cc += dcc;
+      if (oh >= OH) { oh -= OH; ++cc; }
+    }
+    return;
+  }
+  const int kh = static_cast<int>(a.pool_kh), kw = static_cast<int>(a.pool_kw);
+  for (; e < total; e += 256) {
+    const int hs = oh * sh - static_cast<int>(a.pool_ph);
+    const int ws = ow * sw - static_cast<int>(a.pool_pw);
+    const int he = min(hs + kh, Hp), we = min(ws + kw, Wp);
+    const int h0 = max(hs, 0), w0 = max(ws, 0);
+    const float* pl = plane + cc * HpWp;
+    float m = -__builtin_inff();
+    for (int h = h0; h < he; ++h)
+      for (int w = w0; w < we; ++w) {
+        const float v = pl[h * Wp + w];
+        if (v > m || __builtin_isnan(v)) m = v;
+      }
+    yn[e] = m;
+    ow += dow;
+    oh += doh;
+    if (ow >= OW) { ow -= OW; ++oh; }
+    cc += dcc;
+    if (oh >= OH) { oh -= OH; ++cc; }
   }
 }
 
@@ -2409,8 +2482,13 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
                   : 0.f;
   };
   float win[SW][NQ];  // win[t] = channel c - LO + t of the current channel c
+  float sq[SW][NQ];   // its squares, each computed once
 #pragma unroll
-  for (int t = 0; t + 1 < SW; ++t) load(win[t + 1], g0 - LO + t);  // shifted in before use
+  for (int t = 0; t + 1 < SW; ++t) {
+    load(win[t + 1], g0 - LO + t);  // shifted in before use
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) sq[t + 1][i] = win[t + 1][i] * win[t + 1][i];
+  }
   float raw[CB][NQ];  // the lead channels c + LEAD of the block in flight
 #pragma unroll
   for (int j = 0; j < CB; ++j) load(raw[j], g0 + LEAD + j);
@@ -2423,18 +2501,26 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 #pragma unroll
         for (int t = 0; t + 1 < SW; ++t)
 #pragma unroll
-          for (int i = 0; i < NQ; ++i) win[t][i] = win[t + 1][i];
+          for (int i = 0; i < NQ; ++i) {
+            win[t][i] = win[t + 1][i];
+            sq[t][i] = sq[t + 1][i];
+          }
 #pragma unroll
-        for (int i = 0; i < NQ; ++i) win[SW - 1][i] = raw[j][i];
+        for (int i = 0; i < NQ; ++i) {
+          win[SW - 1][i] = raw[j][i];
+          sq[SW - 1][i] = raw[j][i] * raw[j][i];
+        }
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
           const int q = threadIdx.x + 256 * i;
           if (q < HpWp) {
             float v = win[LO][i];
             if constexpr (SIZE > 0) {
-              float sum = 0.f;
+              // ATen's sum from +0 in channel order: a square is never -0,
+              // so +0 + sq[0] is sq[0] and the chain starts there
+              float sum = sq[0][i];
 #pragma unroll
-              for (int t = 0; t < SIZE; ++t) sum = sum + win[t][i] * win[t][i];
+              for (int t = 1; t < SIZE; ++t) sum = sum + sq[t][i];
               if (in[i]) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
             }
             plane[j * HpWp + q] = v;
@@ -2448,8 +2534,8 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
       for (int j = 0; j < CB; ++j) load(raw[j], c0 + CB + LEAD + j);
     }
     __syncthreads();
-    pool_planes(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
-                y + (n * a.C + c0) * OHW);
+    pool_planes_step(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
+                     y + (n * a.C + c0) * OHW);
     __syncthreads();
   }
 }
