@@ -2108,12 +2108,19 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
 
 constexpr int kPoolCB = 16;  // channels per workgroup of the pool pass (register window)
 
+// One image addressed by a buffer descriptor with 32-bit byte offsets (the
+// two register-window pool kernels); larger images take k_pad_lrn_maxpool.
+inline bool pool_image_fits_rsrc(const fedagg_pool_args& a) {
+  return a.C * a.H * a.W < (int64_t(1) << 29);
+}
+
 // Channels per LDS block of the sliding-window pool pass for this chain
 // (k_pad_lrn_maxpool_slide, planes of <= 1024 positions, LRN size 0 / 3 /
 // 4 / 5; <= 24 KiB of LDS), or 0 when the per-block kernels run it (or the
 // caller asks for them with FEDAGG_POOL_PLANES).
 int pool_slide_cb(const fedagg_pool_args& a, int64_t plane) {
   if (a.flags & FEDAGG_POOL_PLANES) return 0;
+  if (!pool_image_fits_rsrc(a)) return 0;
   if (!(a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5))) return 0;
   const int64_t nq = (plane + 255) / 256;
   return nq == 1 ? 16 : nq <= 3 ? 8 : nq == 4 ? 4 : 0;
@@ -2832,6 +2839,7 @@ int fedagg_pool_output(const fedagg_pool_args* a, int64_t* OH, int64_t* OW, int6
     return FEDAGG_EINVAL;
   const int64_t Hp = a->H + a->pad_top + a->pad_bottom, Wp = a->W + a->pad_left + a->pad_right;
   if (Hp >= lim || Wp >= lim || a->C >= (int64_t(1) << 30)) return FEDAGG_EINVAL;
+  if (a->C * a->H * a->W >= (int64_t(1) << 31)) return FEDAGG_EINVAL;  // int offsets per image
   int64_t kh = a->pool_kh, kw = a->pool_kw, sh = a->pool_sh, sw = a->pool_sw;
   int64_t ph = a->pool_ph, pw = a->pool_pw;
   if (kh == 0) {  // no pooling: the padded, normalised planes themselves
@@ -2917,7 +2925,8 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
     }
     return 0;
   }
-  if (nq <= 4 && (a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5))) {
+  if (nq <= 4 && (a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5)) &&
+      pool_image_fits_rsrc(a)) {
     const int64_t nblk = (a.C + CB - 1) / CB;
     for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {  // grid y: at most 65535 images per launch
       const dim3 g(static_cast<unsigned>(nblk),

@@ -243,6 +243,7 @@ def test_conv_and_pool_host_side_shapes(lib):
     for bad in (ops.pool_args((1, 1, 200, 200)),                         # plane > 64 KiB
                 ops.pool_args((1, 1, 8, 8), pool=(2, 2, 2, 2, 2, 0)),    # padding > kernel / 2
                 ops.pool_args((1, 1, 2, 2), pool=(3, 3, 1, 1, 0, 0)),    # kernel > input
-                ops.pool_args((1, 1, 8, 8), (-1, 0, 0, 0))):
+                ops.pool_args((1, 1, 8, 8), (-1, 0, 0, 0)),
+                ops.pool_args((1, 1 << 24, 16, 8))):                     # image >= 2^31 floats
         assert lib.fedagg_pool_output(ctypes.byref(bad), ctypes.byref(oh), ctypes.byref(ow),
                                       ctypes.byref(cb)) == _native.FEDAGG_EINVAL

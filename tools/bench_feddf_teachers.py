@@ -1,7 +1,8 @@
 """FedDF's teacher forwards per distillation batch: the traced replay with
 the Linear layers on the matrix cores (teacher_program.py) against the
 whole-model torch.vmap over the teacher slab, for the reference's model
-shapes (SimpleMLP 784-200-200-10 on MNIST, SimpleCNN2 on CIFAR-100), B = 64
+shapes (SimpleMLP 784-200-200-10 and SimpleCNN on MNIST, SimpleCNN2 on
+CIFAR-100), B = 64
 (the server's test_batch_size), K teachers.  Kernel time from HIP events,
 median of repeated calls.
 
@@ -31,6 +32,25 @@ class SimpleMLP(nn.Module):  # fedsim/models/simple_models.py:23 (Resize is the 
         x = torch.flatten(x, 1)
         x = torch.relu(self.fc1(x))
         x = torch.relu(self.fc2(x))
+        return self.classifier(x)
+
+
+class SimpleCNN(nn.Module):  # fedsim/models/simple_models.py:80-162, MNIST (1 x 28 x 28)
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 32, 5, padding=1)
+        self.conv2 = nn.Conv2d(32, 64, 5, padding=1)
+        self.fc = nn.Linear(64 * 7 * 7, 512)
+        self.classifier = nn.Linear(512, 10)
+
+    def forward(self, x):
+        F = torch.nn.functional
+        x = F.relu(self.conv1(x))
+        x = F.max_pool2d(x, kernel_size=2, stride=2, padding=1)
+        x = F.relu(self.conv2(x))
+        x = F.max_pool2d(x, kernel_size=2, stride=2, padding=1)
+        x = x.view(x.shape[0], -1)
+        x = F.relu(self.fc(x))
         return self.classifier(x)
 
 
@@ -79,12 +99,13 @@ def timed(fn, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--K", default="10,100,1000")
-    ap.add_argument("--models", default="SimpleMLP,SimpleCNN2")
+    ap.add_argument("--models", default="SimpleMLP,SimpleCNN,SimpleCNN2")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-vmap", action="store_true", help="time the replay only")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for name, cls, shape in (("SimpleMLP", SimpleMLP, (64, 1, 28, 28)),
+                             ("SimpleCNN", SimpleCNN, (64, 1, 28, 28)),
                              ("SimpleCNN2", SimpleCNN2, (64, 3, 24, 24))):
         if name not in a.models.split(","):
             continue
