@@ -2017,6 +2017,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  const bool hi = oc0 + 32 < OC;  // wave-uniform
 #pragma unroll
   for (int st = 0; st < RP; ++st) {
     const int r0 = 2 * st, r1 = 2 * st + 1;
@@ -2030,8 +2031,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT
     if (r1 >= R && kk) b0 = b1 = 0.f;  // the zero term of an odd R
     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
     acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    if (hi) {  // the upper 32 output channels exist (SimpleCNN's conv1 has 32)
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
   }
   // epilogue: each bias value loaded once for both pixel groups
   const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;

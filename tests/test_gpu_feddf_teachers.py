@@ -268,6 +268,37 @@ def test_teacher_conv2d_random_shapes_bitwise():
     assert lds_cases >= 5  # the LDS-resident kernel is among them
 
 
+@pytest.mark.parametrize("M,C,H,W,OC,pads,K", [
+    (64, 3, 24, 24, 64, (2, 2, 2, 2), 30),    # SimpleCNN2 conv1
+    (64, 1, 28, 28, 32, (1, 1, 1, 1), 50),    # SimpleCNN conv1: OC = 32, upper half skipped
+    (33, 3, 17, 13, 70, (2, 2, 2, 2), 200),   # ragged last tiles, two channel tiles
+])
+def test_flat_conv_matches_the_gather_chain(M, C, H, W, OC, pads, K):
+    """The 1- / 3-channel LDS conv (every channel staged, k pairs over the
+    flattened (c, kh, kw) index) and the im2col-gather kernel run the same
+    chain: bit for bit over every teacher at the reference's layer sizes;
+    the first and last teacher also against the C oracle."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    g = torch.Generator(device=DEV).manual_seed(M + C + OC + K)
+    kern = (5, 5)
+    R = C * 25
+    P = 3 + OC * R + OC
+    slab = torch.randn(K, P, device=DEV, generator=g)
+    x = torch.randn(M, C, H, W, device=DEV, generator=g)
+    assert ops.conv_order(x.shape, OC, kern, (1, 1), pads) == 0
+    y = ops.teacher_conv2d(x, slab, 3, 3 + OC * R, OC, kern, (1, 1), pads, shared=True, relu=True)
+    yg = ops.teacher_conv2d(x, slab, 3, 3 + OC * R, OC, kern, (1, 1), pads, shared=True,
+                            relu=True, gather=True)
+    assert torch.equal(y.view(torch.int32), yg.view(torch.int32))
+    ends = slab[[0, K - 1]].cpu().numpy()
+    exp = ref.teacher_conv2d(x.cpu().numpy(), ends, 3, 3 + OC * R, OC, kern, (1, 1), pads, True,
+                             True, cc=0)
+    np.testing.assert_array_equal(bits(y[[0, K - 1]].cpu().numpy()), bits(exp))
+
+
 # (shape, pads, lrn, pool)
 POOL_CASES = [
     ((4, 64, 24, 24), (0, 1, 0, 1), (4, 0.001 / 9, 0.75, 1.0), (3, 3, 2, 2, 0, 0)),  # SimpleCNN2 1
