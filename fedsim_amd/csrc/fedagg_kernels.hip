@@ -1456,6 +1456,9 @@ hipError_t with_step(int algo, bool mom, const StepPtrs& sp, F&& f) {
 // chain per output, the bias added last).  Every teacher's weights are read
 // once per 64-row tile: a FedDF batch (64 samples) reads each teacher once.
 // ---------------------------------------------------------------------------
+#ifndef FEDAGG_TL_VEC  // 16-byte staging loads where aligned (A/B builds: 0 = off)
+#define FEDAGG_TL_VEC 1
+#endif
 constexpr int kTL_M = 64;  // output rows (samples) per workgroup
 constexpr int kTL_N = 64;  // output columns (features) per workgroup
 constexpr int kTL_K = 32;  // inputs per LDS stage
@@ -1485,7 +1488,34 @@ __global__ __launch_bounds__(256) void k_teacher_linear(
   // loads are issued into registers before this stage's MFMAs, so their
   // latency hides behind the matrix work.
   float rx[8], rw[8];
+  // 16-byte loads when every row of x and of this teacher's W starts 16-B
+  // aligned (workgroup-uniform): thread t owns inputs 4 (t % 8) .. + 3 of
+  // rows t / 8 + 32 j; else one float per load as e = t + 256 j
+#if FEDAGG_TL_VEC
+  const bool vec = (in % 4) == 0 && (reinterpret_cast<uintptr_t>(xk) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(wk) % 16) == 0;
+#else
+  const bool vec = false;
+#endif
   auto fetch = [&](int64_t i0) {
+    if (vec) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = (t >> 3) + 32 * j;
+        const int64_t i = i0 + 4 * (t & 7);
+        const int64_t m = m0 + r;
+        const int64_t n = n0 + r;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 vx = (m < M && i < in) ? *reinterpret_cast<const f32x4*>(xk + m * in + i) : z;
+        const f32x4 vw = (n < out && i < in) ? *reinterpret_cast<const f32x4*>(wk + n * in + i) : z;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rx[4 * j + q] = vx[q];
+          rw[4 * j + q] = vw[q];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int e = t + 256 * j;
@@ -1499,11 +1529,21 @@ __global__ __launch_bounds__(256) void k_teacher_linear(
   };
   fetch(0);
   for (int64_t i0 = 0; i0 < in; i0 += kTL_K) {
+    if (vec) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = t + 256 * j;
-      sx[e / kTL_K][e % kTL_K] = rx[j];
-      sw[e / kTL_K][e % kTL_K] = rw[j];
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sx[(t >> 3) + 32 * j][4 * (t & 7) + q] = rx[4 * j + q];
+          sw[(t >> 3) + 32 * j][4 * (t & 7) + q] = rw[4 * j + q];
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = t + 256 * j;
+        sx[e / kTL_K][e % kTL_K] = rx[j];
+        sw[e / kTL_K][e % kTL_K] = rw[j];
+      }
     }
     __syncthreads();
     if (i0 + kTL_K < in) fetch(i0 + kTL_K);

@@ -74,6 +74,20 @@ def _pure_forward(model) -> bool:
                    for m in model.modules())
 
 
+def _stack_rows(vectors, device) -> torch.Tensor:
+    """The teachers' flat vectors as the rows of a [K, P] view whose row pitch
+    is padded to 16 bytes, so every teacher's layer weights start where the
+    matrix-core kernels can stage them with 16-byte loads (an odd-P model,
+    e.g. SimpleMLP's 199 210, would otherwise misalign every other row)."""
+    K = len(vectors)
+    P = vectors[0].numel() if K else 0
+    buf = torch.empty((K, (P + 3) // 4 * 4), dtype=torch.float32, device=device)
+    slab = buf[:, :P]
+    for k, t in enumerate(vectors):
+        slab[k].copy_(t.reshape(-1))
+    return slab
+
+
 class TeacherEnsemble(object):
     """K teacher parameter vectors stacked in one slab; ``mean_logits(x)`` is
     the reference's weight-1 SerialAggregator average of their outputs."""
@@ -81,7 +95,7 @@ class TeacherEnsemble(object):
     def __init__(self, model, teacher_vectors, device, program=True):
         self.model = model
         self.named = list(model.named_parameters())
-        self.slab = torch.stack([t.reshape(-1) for t in teacher_vectors]).to(device)
+        self.slab = _stack_rows(teacher_vectors, device)
         self.K = self.slab.shape[0]
         self.batched = (self.slab.device.type == "cuda"
                         and len(list(model.buffers())) == 0)

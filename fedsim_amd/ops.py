@@ -378,6 +378,16 @@ def unpack_row(Xb: torch.Tensor, r: int, P: int, out: Optional[torch.Tensor] = N
     return out
 
 
+def _rows_contiguous(slab: torch.Tensor) -> bool:
+    """[K, P] with unit column stride and a row pitch >= P (a slab whose rows
+    are padded to 16 B, as TeacherEnsemble allocates it)."""
+    return slab.stride(1) == 1 and (slab.shape[0] <= 1 or slab.stride(0) >= slab.shape[1])
+
+
+def _row_pitch(slab: torch.Tensor) -> int:
+    return slab.stride(0) if slab.shape[0] > 1 else slab.shape[1]
+
+
 def teacher_linear(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int, in_f: int,
                    out_f: int, shared: bool, relu: bool = False) -> torch.Tensor:
     """One nn.Linear layer of the K teacher models whose flat parameter
@@ -387,8 +397,8 @@ def teacher_linear(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int, 
     (ReLU applied when ``relu``).  b_off = -1: no bias."""
     _require_hip_f32(x, "x")
     _require_hip_f32(slab, "slab")
-    if slab.dim() != 2 or not slab.is_contiguous() or x.device != slab.device:
-        raise ValueError("slab must be a contiguous [K, P] tensor on x's device")
+    if slab.dim() != 2 or not _rows_contiguous(slab) or x.device != slab.device:
+        raise ValueError("slab must be a [K, P] tensor with contiguous rows on x's device")
     if not x.is_contiguous() or x.shape[-1] != in_f:
         raise ValueError(f"x must be contiguous with a last dimension of {in_f}")
     K, P = slab.shape
@@ -399,8 +409,8 @@ def teacher_linear(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int, 
         raise ValueError("a per-teacher x must have K rows in its first dimension")
     y = torch.empty((K, M, out_f), dtype=torch.float32, device=x.device)
     rc = _native.load().fedagg_teacher_linear_f32(
-        x.data_ptr(), 0 if shared else M * in_f, slab.data_ptr(), P, w_off, b_off, K, M, in_f,
-        out_f, y.data_ptr(), _native.FEDAGG_RELU if relu else 0, _stream_ptr(x.device))
+        x.data_ptr(), 0 if shared else M * in_f, slab.data_ptr(), _row_pitch(slab), w_off, b_off,
+        K, M, in_f, out_f, y.data_ptr(), _native.FEDAGG_RELU if relu else 0, _stream_ptr(x.device))
     check(rc, "fedagg_teacher_linear_f32")
     return y
 
@@ -438,8 +448,8 @@ def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
     ``gather``: the im2col-gather kernel even where the LDS one applies."""
     _require_hip_f32(x, "x")
     _require_hip_f32(slab, "slab")
-    if slab.dim() != 2 or not slab.is_contiguous() or x.device != slab.device:
-        raise ValueError("slab must be a contiguous [K, P] tensor on x's device")
+    if slab.dim() != 2 or not _rows_contiguous(slab) or x.device != slab.device:
+        raise ValueError("slab must be a [K, P] tensor with contiguous rows on x's device")
     K, P = slab.shape
     if not x.is_contiguous() or x.dim() != (4 if shared else 5):
         raise ValueError("x must be a contiguous [M, C, H, W] (shared) or [K, M, C, H, W] tensor")
@@ -459,8 +469,8 @@ def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
     shape = _native.Conv2dShape(M, C, H, W, out_channels, KH, KW, sh, sw, pt, pl, OH, OW)
     y = torch.empty((K, M, out_channels, OH, OW), dtype=torch.float32, device=x.device)
     rc = _native.load().fedagg_teacher_conv2d_f32(
-        x.data_ptr(), 0 if shared else M * C * H * W, slab.data_ptr(), P, w_off, b_off, K,
-        ctypes.byref(shape), y.data_ptr(),
+        x.data_ptr(), 0 if shared else M * C * H * W, slab.data_ptr(), _row_pitch(slab), w_off,
+        b_off, K, ctypes.byref(shape), y.data_ptr(),
         (_native.FEDAGG_RELU if relu else 0) | (_native.FEDAGG_CONV_GATHER if gather else 0),
         _stream_ptr(x.device))
     check(rc, "fedagg_teacher_conv2d_f32")

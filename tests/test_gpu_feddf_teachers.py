@@ -123,6 +123,53 @@ def test_teacher_linear_kernel_is_the_fmaf_chain(M, in_f, out_f, shared):
         np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp))
 
 
+@pytest.mark.parametrize("w_off,P_pad", [(0, 0), (4, 0), (8, 2), (0, 1)])
+def test_teacher_linear_aligned_rows_bitwise(w_off, P_pad):
+    """16-byte staging loads (rows of x and of the teacher's W 16-B aligned;
+    with P % 4 = 2 every other teacher takes the 4-byte loads): bitwise vs
+    the C oracle's fmaf chain at SimpleMLP's and SimpleCNN's layer sizes."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    for M, in_f, out_f in ((64, 784, 200), (64, 3136, 80), (70, 32, 130)):
+        g = torch.Generator(device=DEV).manual_seed(in_f + out_f + w_off + P_pad)
+        K = 4
+        P = (w_off + in_f * out_f + out_f + 3) // 4 * 4 + P_pad
+        slab = torch.randn(K, P, device=DEV, generator=g)
+        for shared in (True, False):
+            x = torch.randn((M, in_f) if shared else (K, M, in_f), device=DEV, generator=g)
+            y = ops.teacher_linear(x, slab, w_off, w_off + in_f * out_f, in_f, out_f,
+                                   shared=shared, relu=True)
+            exp = ref.teacher_linear(x.cpu().numpy(), slab.cpu().numpy(), w_off,
+                                     w_off + in_f * out_f, in_f, out_f, shared, True)
+            np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(exp))
+
+
+def test_padded_row_pitch_slab_same_bits():
+    """TeacherEnsemble pads each teacher's row to 16 bytes; the Linear and
+    Conv2d kernels read a row-strided [K, P] view (row pitch passed as the
+    teachers' stride) with the same results as a contiguous slab."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from fedsim_amd.distributed.centralized.training.feddf import _stack_rows
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    K, P = 5, 199_210  # SimpleMLP's P: odd rows misaligned in a contiguous slab
+    rows = [torch.randn(P, device=DEV, generator=g) for _ in range(K)]
+    padded = _stack_rows(rows, DEV)
+    assert padded.stride(0) % 4 == 0 and padded.stride(0) >= P
+    dense = torch.stack(rows)
+    x = torch.randn(64, 784, device=DEV, generator=g)
+    a = ops.teacher_linear(x, padded, 0, 784 * 200, 784, 200, shared=True, relu=True)
+    b = ops.teacher_linear(x, dense, 0, 784 * 200, 784, 200, shared=True, relu=True)
+    np.testing.assert_array_equal(bits(a.cpu().numpy()), bits(b.cpu().numpy()))
+    xc = torch.randn(8, 3, 24, 24, device=DEV, generator=g)
+    a = ops.teacher_conv2d(xc, padded, 1, 4801, 64, (5, 5), (1, 1), (2, 2, 2, 2), shared=True)
+    b = ops.teacher_conv2d(xc, dense, 1, 4801, 64, (5, 5), (1, 1), (2, 2, 2, 2), shared=True)
+    np.testing.assert_array_equal(bits(a.cpu().numpy()), bits(b.cpu().numpy()))
+
+
 def test_teacher_linear_random_shapes_bitwise():
     """Random layer shapes, offsets and teacher counts (seeded), bitwise vs
     the C oracle's fmaf chain, including special values in the inputs."""
