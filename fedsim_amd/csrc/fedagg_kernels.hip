@@ -2135,7 +2135,11 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
       if (p->lds <= 64 * 1024) return true;
     }
   }
-  const int cc = s.C >= 4 ? 4 : 2;
+#ifndef FEDAGG_CONV_CC2_XM16  // A/B builds: 1 = chunks of 2 channels where 4 need 16 staging regs
+#define FEDAGG_CONV_CC2_XM16 0
+#endif
+  int cc = s.C >= 4 ? 4 : 2;
+  if (FEDAGG_CONV_CC2_XM16 && cc == 4 && cc * nslot * HW > 8 * 256) cc = 2;
   const int64_t xtot = cc * nslot * HW;
   const int xm = xtot <= 8 * 256 ? 8 : 16;
   if (xtot > xm * 256) return false;
