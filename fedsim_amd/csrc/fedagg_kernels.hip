@@ -2135,9 +2135,9 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
       if (p->lds <= 64 * 1024) return true;
     }
   }
-#ifndef FEDAGG_CONV_CC2_XM16  // A/B builds: 1 = chunks of 2 channels where 4 need 16 staging regs
-#define FEDAGG_CONV_CC2_XM16 0
-#endif
+#ifndef FEDAGG_CONV_CC2_XM16  // chunks of 2 channels where 4 would need 16 staging registers
+#define FEDAGG_CONV_CC2_XM16 1  // (SimpleCNN conv2, 32 ch at 14x14: whole teacher batch at
+#endif                          // K=1000 14.55 -> 13.97 ms, profiles/r02xa; 0 for A/B builds)
   int cc = s.C >= 4 ? 4 : 2;
   if (FEDAGG_CONV_CC2_XM16 && cc == 4 && cc * nslot * HW > 8 * 256) cc = 2;
   const int64_t xtot = cc * nslot * HW;
