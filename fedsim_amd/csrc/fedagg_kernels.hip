@@ -1958,11 +1958,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // (fedagg_conv_order 0, oracle ref_teacher_conv2d_f32 with cc = 0): a
 // trailing +0 term leaves a chain that never holds -0 unchanged.
 // ---------------------------------------------------------------------------
+#ifndef FEDAGG_FLAT_WAVES  // waves per workgroup of the flat conv, 64 output pixels each (A/B
+#define FEDAGG_FLAT_WAVES 4   // builds: 8 stages each image once per 512 pixels but runs two
+#endif                        // workgroups per CU; conv1 2.33 vs 2.13 ms, profiles/r02xf)
+constexpr int kFlatThreads = 64 * FEDAGG_FLAT_WAVES;
 #ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds;
 #define FEDAGG_FLAT_WPE 4  // 4: SimpleCNN2 conv1 2.26 ms vs 2.52 ms with 3, profiles/r02x3)
 #endif
 template <int KS, int CI, int XM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
+__global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
     float* __restrict__ y, int relu) {
@@ -1987,7 +1991,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT
   const int HW = H * W;
   const int NPX = static_cast<int>(s.M) * OHW;
   const int OC = static_cast<int>(s.OC);
-  const int px0 = pxt * kTC_PX;
+  const int px0 = pxt * kFlatThreads;  // one 64-pixel column pair per wave
   const int m_lo = px0 / OHW;
   const int pt = static_cast<int>(s.pad_h), pl = static_cast<int>(s.pad_w);
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
@@ -2000,11 +2004,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT
   // stage every channel of the tile's images: element e = t + 256 i is
   // (slot, channel, hw) in the input's own order, i.e. global offset e
   const int xtot = nslot * CI * HW;
-  for (int i = t; i < nslot * CI * HpWp; i += 256) sX[i] = 0.f;
+  for (int i = t; i < nslot * CI * HpWp; i += kFlatThreads) sX[i] = 0.f;
   float rx[XM];
 #pragma unroll
   for (int i = 0; i < XM; ++i) {
-    const int e = t + 256 * i;
+    const int e = t + kFlatThreads * i;
     rx[i] = e < xtot ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                  xres, static_cast<int>(e * 4u + x_tile4), 0, 0))
                      : 0.f;
@@ -2017,13 +2021,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT
   float rw[WPT];
 #pragma unroll
   for (int i = 0; i < WPT; ++i)
-    rw[i] = (wq + 4 * i < R) ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+    rw[i] = (t < 256 && wq + 4 * i < R) ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                      wres, static_cast<int>(wg4 + 16u * i), 0, 0))
                              : 0.f;
   __syncthreads();  // halo zeroes before the planes land
 #pragma unroll
   for (int i = 0; i < XM; ++i) {
-    const int e = t + 256 * i;
+    const int e = t + kFlatThreads * i;
     if (e < xtot) {
       const int sc = e / HW;  // slot * CI + channel
       const int hw = e - sc * HW;
@@ -2034,7 +2038,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT
   }
 #pragma unroll
   for (int i = 0; i < WPT; ++i)
-    if (wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
+    if (t < 256 && wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
   __syncthreads();
   const int col = lane & 31;
   const int kk = lane >> 5;
@@ -2124,14 +2128,16 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
   int64_t nslot = (kTC_PX - 2) / OHW + 2;
   if (nslot > s.M) nslot = s.M;
   if (s.C == 1 || s.C == 3) {  // every channel staged at once (k_teacher_conv2d_flat)
-    const int64_t xall = s.C * nslot * HW;
-    if (xall <= 16 * 256) {
+    int64_t fslot = (kFlatThreads - 2) / OHW + 2;
+    if (fslot > s.M) fslot = s.M;
+    const int64_t xall = s.C * fslot * HW;
+    if (xall <= 16 * kFlatThreads) {
       const int64_t rw = (s.C * ks * ks + 1) / 2 * 2 + 1;
       p->ks = static_cast<int>(ks);
       p->cc = 0;
-      p->xm = xall <= 8 * 256 ? 8 : 16;
-      p->nslot = static_cast<int>(nslot);
-      p->lds = static_cast<size_t>(kTC_OC * rw + nslot * s.C * Hp * Wp) * sizeof(float);
+      p->xm = xall <= 8 * kFlatThreads ? 8 : 16;
+      p->nslot = static_cast<int>(fslot);
+      p->lds = static_cast<size_t>(kTC_OC * rw + fslot * s.C * Hp * Wp) * sizeof(float);
       if (p->lds <= 64 * 1024) return true;
     }
   }
@@ -2823,9 +2829,11 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   hipLaunchKernelGGL((k_teacher_conv2d_lds<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
 #define FEDAGG_CONV_FLAT(KS, CI, XM)                                                          \
-  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM>), grid, dim3(256), plan.lds, st, xk, \
+  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM>), gflat, dim3(kFlatThreads), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
       if (plan.cc == 0) {
+        const dim3 gflat(static_cast<unsigned>((s.M * s.OH * s.OW + kFlatThreads - 1) / kFlatThreads),
+                         static_cast<unsigned>(oc_tiles), static_cast<unsigned>(kn));
         if (plan.ks == 5) {
           if (s.C == 3) {
             if (plan.xm == 8) FEDAGG_CONV_FLAT(5, 3, 8); else FEDAGG_CONV_FLAT(5, 3, 16);
