@@ -2002,16 +2002,37 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
       const_cast<float*>(params + k * params_kstride + w_off), static_cast<short>(0),
       OC * R * 4, 0x00020000);
   // stage every channel of the tile's images: element e = t + 256 i is
-  // (slot, channel, hw) in the input's own order, i.e. global offset e
+  // (slot, channel, hw) in the input's own order, i.e. global offset e.
+  // Only the padded rows the tile's output rows read are staged (and
+  // zeroed): from row_lo of the first image to row_hi of the last one
+  // (a 256-pixel tile needs ~1/3 of the two 24 x 24 images it touches).
   const int xtot = nslot * CI * HW;
-  for (int i = t; i < nslot * CI * HpWp; i += kFlatThreads) sX[i] = 0.f;
+  const int pend = (px0 + kFlatThreads < NPX ? px0 + kFlatThreads : NPX) - 1;
+  const int last = pend / OHW - m_lo;  // slot of the tile's last image
+  const int row_lo = (px0 - m_lo * OHW) / OW;
+  const int row_hi = (pend - (m_lo + last) * OHW) / OW + KS - 1;
+  for (int pc = 0; pc < (last + 1) * CI; ++pc) {
+    const int slot = pc / CI;
+    const int lo = slot == 0 ? row_lo : 0;
+    const int hi = slot == last ? row_hi : Hp - 1;
+    for (int q = lo * Wp + t; q < (hi + 1) * Wp; q += kFlatThreads) sX[pc * HpWp + q] = 0.f;
+  }
   float rx[XM];
+  int lidx[XM];
 #pragma unroll
   for (int i = 0; i < XM; ++i) {
     const int e = t + kFlatThreads * i;
-    rx[i] = e < xtot ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 xres, static_cast<int>(e * 4u + x_tile4), 0, 0))
-                     : 0.f;
+    const int sc = e / HW;  // slot * CI + channel
+    const int slot = sc / CI;
+    const int hw = e - sc * HW;
+    const int h = hw / W;
+    const int prow = h + pt;
+    const bool need = e < xtot && slot <= last && (slot > 0 || prow >= row_lo) &&
+                      (slot < last || prow <= row_hi);
+    lidx[i] = need ? (sc * Hp + prow) * Wp + (hw - h * W) + pl : -1;
+    rx[i] = need ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                          xres, static_cast<int>(e * 4u + x_tile4), 0, 0))
+                 : 0.f;
   }
   // weights: thread t owns output channel oc0 + t / 4, columns t % 4 + 4 i
   // (columns past R, and rows past OC, are zero)
@@ -2026,16 +2047,8 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
                              : 0.f;
   __syncthreads();  // halo zeroes before the planes land
 #pragma unroll
-  for (int i = 0; i < XM; ++i) {
-    const int e = t + kFlatThreads * i;
-    if (e < xtot) {
-      const int sc = e / HW;  // slot * CI + channel
-      const int hw = e - sc * HW;
-      const int h = hw / W;
-      const int w = hw - h * W;
-      sX[(sc * Hp + h + pt) * Wp + w + pl] = rx[i];
-    }
-  }
+  for (int i = 0; i < XM; ++i)
+    if (lidx[i] >= 0) sX[lidx[i]] = rx[i];
 #pragma unroll
   for (int i = 0; i < WPT; ++i)
     if (t < 256 && wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
