@@ -248,3 +248,40 @@ def test_conv_and_pool_host_side_shapes(lib):
                 ops.pool_args((1, 1 << 24, 16, 8))):                     # image >= 2^31 floats
         assert lib.fedagg_pool_output(ctypes.byref(bad), ctypes.byref(oh), ctypes.byref(ow),
                                       ctypes.byref(cb)) == _native.FEDAGG_EINVAL
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """Every struct include/fedagg.h declares has the same size and field
+    offsets in the ctypes binding as in C (compiled here with gcc against the
+    header), e.g. fedagg_pool_args' flags in the former padding after lrn_k."""
+    import ctypes
+    import shutil
+    import subprocess
+
+    from fedsim_amd import _native
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {
+        "fedagg_pool_args": _native.PoolArgs,
+        "fedagg_conv2d_shape": _native.Conv2dShape,
+        "fedagg_sgd_params": _native.SgdParams,
+        "fedagg_step_args": _native.StepArgs,
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fedagg.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for field, _ in py._fields_:
+            lines.append(f'  printf("{cname} {field} %zu\\n", offsetof({cname}, {field}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(ln.split()[:2]): int(ln.split()[2]) for ln in out if ln.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for field, _ in py._fields_:
+            assert got[(cname, field)] == getattr(py, field).offset, (cname, field)
