@@ -1965,7 +1965,7 @@ constexpr int kFlatThreads = 64 * FEDAGG_FLAT_WAVES;
 #ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds;
 #define FEDAGG_FLAT_WPE 4  // 4: SimpleCNN2 conv1 2.26 ms vs 2.52 ms with 3, profiles/r02x3)
 #endif
-template <int KS, int CI, int XM>
+template <int KS, int CI, int XM, bool HALF>
 __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
@@ -1975,6 +1975,11 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   constexpr int RP = (R + 1) / 2;    // k steps
   constexpr int RW = 2 * RP + 1;     // sW row pitch (odd)
   constexpr int WPT = (2 * RP + 3) / 4;
+  // HALF (OC <= 32: the upper 32 output channels of the MFMA tile do not
+  // exist): the second accumulator pair takes two more 32-pixel groups
+  // instead, so a wave owns 128 pixels and the tile 512
+  constexpr int NPG = HALF ? 4 : 2;          // 32-pixel groups per wave
+  constexpr int TPX = 32 * NPG * (kFlatThreads / 64);
   extern __shared__ float lds[];
   float* sW = lds;
   float* sX = lds + kTC_OC * RW;
@@ -1991,7 +1996,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int HW = H * W;
   const int NPX = static_cast<int>(s.M) * OHW;
   const int OC = static_cast<int>(s.OC);
-  const int px0 = pxt * kFlatThreads;  // one 64-pixel column pair per wave
+  const int px0 = pxt * TPX;
   const int m_lo = px0 / OHW;
   const int pt = static_cast<int>(s.pad_h), pl = static_cast<int>(s.pad_w);
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
@@ -2007,7 +2012,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   // zeroed): from row_lo of the first image to row_hi of the last one
   // (a 256-pixel tile needs ~1/3 of the two 24 x 24 images it touches).
   const int xtot = nslot * CI * HW;
-  const int pend = (px0 + kFlatThreads < NPX ? px0 + kFlatThreads : NPX) - 1;
+  const int pend = (px0 + TPX < NPX ? px0 + TPX : NPX) - 1;
   const int last = pend / OHW - m_lo;  // slot of the tile's last image
   const int row_lo = (px0 - m_lo * OHW) / OW;
   const int row_hi = (pend - (m_lo + last) * OHW) / OW + KS - 1;
@@ -2056,10 +2061,10 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int col = lane & 31;
   const int kk = lane >> 5;
   const float* pa = sW + col * RW + kk;
-  int xb[2];
+  int xb[NPG];
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    int p = px0 + wave * 64 + b * 32 + col;
+  for (int b = 0; b < NPG; ++b) {
+    int p = px0 + wave * 32 * NPG + b * 32 + col;
     p = p < NPX ? p : NPX - 1;
     const int m = p / OHW;
     const int ohw = p - m * OHW;
@@ -2074,7 +2079,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-  const bool hi = oc0 + 32 < OC;  // wave-uniform
+  [[maybe_unused]] const bool hi = oc0 + 32 < OC;  // wave-uniform
 #pragma unroll
   for (int st = 0; st < RP; ++st) {
     const int r0 = 2 * st, r1 = 2 * st + 1;
@@ -2082,40 +2087,50 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
     const int o1 = r1 < R ? (r1 / TAPS) * HpWp + ((r1 % TAPS) / KS) * Wp + r1 % KS : 0;
     const int ob = kk ? o1 : o0;
     const float a0 = pa[2 * st];
-    const float a1 = pa[32 * RW + 2 * st];
-    float b0 = sX[xb[0] + ob];
-    float b1 = sX[xb[1] + ob];
-    if (r1 >= R && kk) b0 = b1 = 0.f;  // the zero term of an odd R
-    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-    if (hi) {  // the upper 32 output channels exist (SimpleCNN's conv1 has 32)
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    float bv[NPG];
+#pragma unroll
+    for (int b = 0; b < NPG; ++b) bv[b] = sX[xb[b] + ob];
+    if (r1 >= R && kk) {  // the zero term of an odd R
+#pragma unroll
+      for (int b = 0; b < NPG; ++b) bv[b] = 0.f;
+    }
+    if constexpr (HALF) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        acc[g >> 1][g & 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[g], acc[g >> 1][g & 1], 0, 0, 0);
+    } else {
+      const float a1 = pa[32 * RW + 2 * st];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[0], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[1], acc[0][1], 0, 0, 0);
+      if (hi) {  // the upper 32 output channels exist
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[0], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[1], acc[1][1], 0, 0, 0);
+      }
     }
   }
   // epilogue: each bias value loaded once for both pixel groups
   const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
-  float* yp[2];
-  bool pin[2];
+  float* yp[NPG];
+  bool pin[NPG];
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int p = px0 + wave * 64 + b * 32 + col;
+  for (int b = 0; b < NPG; ++b) {
+    const int p = px0 + wave * 32 * NPG + b * 32 + col;
     pin[b] = p < NPX;
     const int pc = pin[b] ? p : 0;
     const int m = pc / OHW;
     yp[b] = y + (k * s.M + m) * s.OC * OHW + (pc - m * OHW);
   }
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
+  for (int a = 0; a < (HALF ? 1 : 2); ++a) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
       if (oc >= OC) continue;
       const float bias = bk ? bk[oc] : 0.f;
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < NPG; ++b) {
         if (!pin[b]) continue;
-        float v = acc[a][b][e] + bias;
+        float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias;
         if (relu) v = v > 0.f ? v : 0.f;
         yp[b][int64_t(oc) * OHW] = v;
       }
@@ -2141,7 +2156,8 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
   int64_t nslot = (kTC_PX - 2) / OHW + 2;
   if (nslot > s.M) nslot = s.M;
   if (s.C == 1 || s.C == 3) {  // every channel staged at once (k_teacher_conv2d_flat)
-    int64_t fslot = (kFlatThreads - 2) / OHW + 2;
+    const int64_t tpx = (s.OC <= 32 ? 2 : 1) * kFlatThreads;  // HALF tiles: 512 pixels
+    int64_t fslot = (tpx - 2) / OHW + 2;
     if (fslot > s.M) fslot = s.M;
     const int64_t xall = s.C * fslot * HW;
     if (xall <= 16 * kFlatThreads) {
@@ -2842,10 +2858,16 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   hipLaunchKernelGGL((k_teacher_conv2d_lds<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
 #define FEDAGG_CONV_FLAT(KS, CI, XM)                                                          \
-  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM>), gflat, dim3(kFlatThreads), plan.lds, st, xk, \
+  do {                                                                                        \
+    if (half) FEDAGG_CONV_FLAT_H(KS, CI, XM, true); else FEDAGG_CONV_FLAT_H(KS, CI, XM, false); \
+  } while (0)
+#define FEDAGG_CONV_FLAT_H(KS, CI, XM, HF)                                                    \
+  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM, HF>), gflat, dim3(kFlatThreads), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
       if (plan.cc == 0) {
-        const dim3 gflat(static_cast<unsigned>((s.M * s.OH * s.OW + kFlatThreads - 1) / kFlatThreads),
+        const bool half = s.OC <= 32;
+        const int64_t tpx = (half ? 2 : 1) * kFlatThreads;
+        const dim3 gflat(static_cast<unsigned>((s.M * s.OH * s.OW + tpx - 1) / tpx),
                          static_cast<unsigned>(oc_tiles), static_cast<unsigned>(kn));
         if (plan.ks == 5) {
           if (s.C == 3) {
@@ -2874,6 +2896,7 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
         }
       }
 #undef FEDAGG_CONV_FLAT
+#undef FEDAGG_CONV_FLAT_H
 #undef FEDAGG_CONV_LDS
       const int rc = static_cast<int>(hipGetLastError());
       if (rc) return rc;

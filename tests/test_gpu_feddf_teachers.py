@@ -319,6 +319,7 @@ def test_teacher_conv2d_random_shapes_bitwise():
     (64, 3, 24, 24, 64, (2, 2, 2, 2), 30),    # SimpleCNN2 conv1
     (64, 1, 28, 28, 32, (1, 1, 1, 1), 50),    # SimpleCNN conv1: OC = 32, upper half skipped
     (33, 3, 17, 13, 70, (2, 2, 2, 2), 200),   # ragged last tiles, two channel tiles
+    (9, 3, 20, 20, 20, (2, 2, 2, 2), 40),     # OC <= 32: 128 pixels per wave, ragged
 ])
 def test_flat_conv_matches_the_gather_chain(M, C, H, W, OC, pads, K):
     """The 1- / 3-channel LDS conv (every channel staged, k pairs over the
