@@ -1761,8 +1761,11 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
 constexpr int kTC_XPK_LDS = 14;  // LDS float index bits of a packed staging offset
 constexpr int kTC_XPK_GLB = 18;  // global float offset bits
 
+#ifndef FEDAGG_LDS_WPE  // waves per SIMD the chunked conv is compiled for (A/B builds; 4
+#define FEDAGG_LDS_WPE 3   // spills 57 VGPRs: SimpleCNN2 conv2 7.50 vs 6.92 ms, profiles/r02xi)
+#endif
 template <int KS, int CC, int XM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_lds(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_LDS_WPE, FEDAGG_LDS_WPE))) void k_teacher_conv2d_lds(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
     float* __restrict__ y, int relu) {
