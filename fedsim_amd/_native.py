@@ -23,7 +23,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
 
 # Must match include/fedagg.h
-ABI_VERSION = 1
+ABI_VERSION = 2  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row)
 FEDAGG_INIT = 0x1
 FEDAGG_FINALIZE = 0x2
 FEDAGG_NT = 0x4
@@ -233,12 +233,22 @@ def load():
                 f"'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
             )
         lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        # the version first: a library built before an entry point existed
+        # must fail with this message, not at the symbol lookup
+        lib.fedagg_abi_version.restype = ctypes.c_int
+        lib.fedagg_abi_version.argtypes = []
+        built = lib.fedagg_abi_version()
+        if built != ABI_VERSION:
+            raise FedAggError(f"{LIB_PATH} has ABI version {built}, this package needs "
+                              f"{ABI_VERSION}; rebuild the library")
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                raise FedAggError(f"{LIB_PATH} does not export {name}; rebuild the library") \
+                    from None
             fn.restype = res
             fn.argtypes = args
-        if lib.fedagg_abi_version() != ABI_VERSION:
-            raise FedAggError("libfedagg ABI version mismatch; rebuild the library")
         runtimes = _hip_runtimes_mapped()
         if len(runtimes) > 1:
             raise FedAggError(

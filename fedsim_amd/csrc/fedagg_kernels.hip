@@ -2797,13 +2797,22 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
   if (!x || !params || !y) return FEDAGG_EINVAL;
   const int64_t n_tiles = (out + kTL_N - 1) / kTL_N;
   const int64_t m_tiles = (M + kTL_M - 1) / kTL_M;
-  const int64_t tiles = K * n_tiles * m_tiles;
-  if (tiles > (int64_t(1) << 31) - 1) return FEDAGG_EINVAL;
-  hipLaunchKernelGGL(k_teacher_linear, dim3(static_cast<unsigned>(tiles)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), x, x_kstride, params, params_kstride,
-                     w_off, b_off, M, in, out, y, n_tiles, m_tiles,
-                     (flags & FEDAGG_RELU) ? 1 : 0);
-  return static_cast<int>(hipGetLastError());
+  // a 1-D grid: gridDim.x * blockDim.x must stay below 2^32, so the teachers
+  // go in chunks of at most kMaxGridX / (tiles per teacher) per launch
+  const int64_t per = n_tiles * m_tiles;
+  const int64_t kMaxGridX = (int64_t(1) << 32) / 256 - 1;
+  if (per > kMaxGridX) return FEDAGG_EINVAL;
+  const int64_t kchunk = kMaxGridX / per;
+  for (int64_t k0 = 0; k0 < K; k0 += kchunk) {
+    const int64_t kn = K - k0 < kchunk ? K - k0 : kchunk;
+    hipLaunchKernelGGL(k_teacher_linear, dim3(static_cast<unsigned>(kn * per)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), x + k0 * x_kstride, x_kstride,
+                       params + k0 * params_kstride, params_kstride, w_off, b_off, M, in, out,
+                       y + k0 * M * out, n_tiles, m_tiles, (flags & FEDAGG_RELU) ? 1 : 0);
+    const int rc = static_cast<int>(hipGetLastError());
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int fedagg_conv_stage(int64_t R) {
@@ -2845,7 +2854,8 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   if (!x || !params || !y) return FEDAGG_EINVAL;
   const int64_t oc_tiles = (s.OC + kTC_OC - 1) / kTC_OC;
   const int64_t px_tiles = (s.M * s.OH * s.OW + kTC_PX - 1) / kTC_PX;
-  if (px_tiles > (int64_t(1) << 31) - 1 || oc_tiles > 65535) return FEDAGG_EINVAL;
+  // gridDim.x * blockDim.x below 2^32 (256-lane tiles; the flat kernel's grid is no wider)
+  if (px_tiles > (int64_t(1) << 32) / 256 - 1 || oc_tiles > 65535) return FEDAGG_EINVAL;
   const int relu = (flags & FEDAGG_RELU) ? 1 : 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   ConvLdsPlan plan;
@@ -3022,6 +3032,7 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
   if (nq <= 4 && (a.lrn_size == 0 || (a.lrn_size >= 3 && a.lrn_size <= 5)) &&
       pool_image_fits_rsrc(a)) {
     const int64_t nblk = (a.C + CB - 1) / CB;
+    if (nblk > (int64_t(1) << 32) / 256 - 1) return FEDAGG_EINVAL;
     for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {  // grid y: at most 65535 images per launch
       const dim3 g(static_cast<unsigned>(nblk),
                    static_cast<unsigned>(a.N - n0 < 65535 ? a.N - n0 : 65535));

@@ -8,29 +8,43 @@ as teachers, their logits averaged through a SerialAggregator with weight 1
 (feddf.py:117-122), and the cloud model takes one server-optimizer step on the
 KL divergence to that average (feddf.py:124-140).
 
-MI355X-first differences (same results):
+MI355X-first differences:
 
 * The reference re-copies every teacher into the model for every batch
   (``initialize_module``, K x P bytes per batch).  Here the K teacher vectors
-  are stacked once per round into one [K, P] HBM slab and each teacher runs
-  through ``functional_call`` on views of its row.
+  are stacked once per round into one [K, P] HBM slab.
 * On a HIP device, and for models without buffers, the K teacher forwards run
   as ONE batched forward into a [K, B*C] logits slab: the model's traced graph
-  replayed over all K teachers, its ``nn.Linear`` layers on the matrix cores
-  (``fedagg_teacher_linear_f32``, v_mfma_f32_16x16x4_f32, ReLU fused;
-  teacher_program.py) and the rest under ``torch.vmap``; a model that does
-  not trace keeps the whole-model ``vmap`` over the slab rows (chunked to
-  bound activation memory).  The teacher
-  average is one launch of the exact-mode reduce kernel
-  (``fedagg_reduce_f32``, weights 1, divide by fl32(K)): the same per-element
-  arithmetic and order as the reference's ``add(target, 1)`` x K + ``get``.
+  replayed over all K teachers (teacher_program.py) -- every ``nn.Linear``
+  (``fedagg_teacher_linear_f32``, v_mfma_f32_16x16x4_f32) and ``nn.Conv2d``
+  (``fedagg_teacher_conv2d_f32``, v_mfma_f32_32x32x2_f32 implicit GEMM) on
+  the matrix cores with a following ReLU fused, every zero-pad / LRN /
+  max-pool chain as one pass (``fedagg_pad_lrn_maxpool_f32``), the remaining
+  nodes under ``torch.vmap`` and parameterless foreign leaves (the reference
+  models' ``Resize``) once per batch.  The teacher average is one launch of
+  the exact-mode reduce kernel (``fedagg_reduce_f32``, weights 1, divide by
+  fl32(K)): the reference's ``add(target, 1)`` x K + ``get`` arithmetic and
+  order on the same logits.
+* Parity is normwise, not bitwise, on this path: the matrix-core layers sum
+  each output as one fmaf chain (not the CPU GEMM's order) and the LRN power
+  is exp2/log2, a few ulps from powf.  The replay is checked against the
+  whole-model ``vmap`` on its first batch (normwise 1e-4) and pinned to the
+  reference's own SimpleCNN2 / SimpleCNN FedDF rounds
+  (tests/golden/feddf_cnn.*, tests/test_gpu_feddf_cnn.py).
+* Whenever the replay is not used -- the forward does not trace, a kernel
+  raises, or the first-batch check fails -- the ensemble falls back to the
+  whole-model ``vmap`` (and, when that raises too, e.g. on random ops, to
+  the reference's one-teacher-at-a-time loop), warns once with the reason and
+  counts it: ``TeacherEnsemble.fallbacks`` / ``fallback_reason``, and per
+  round in the server storage entry ``"teacher_replay"`` (with the kernel
+  launch counts).
 * The teachers are fixed for the whole distillation (they are this round's
-  client models) and the server's dataloaders do not shuffle, so the
-  ensemble's mean logits of each batch are computed in the first epoch and
-  reused by the later ones (``global_epochs`` > 1) when the model's forward
-  is pure (no buffers to update, no dropout): the same batches, the same
-  forwards, the same bits, one teacher pass per round instead of one per
-  epoch.
+  client models), so when the loader does not shuffle and the forward is a
+  pure function of (teacher, input) -- no buffers, no dropout, no random
+  op in the traced graph -- the ensemble's mean logits of each batch are
+  computed in the first epoch and reused by the later ones (``global_epochs``
+  > 1), after checking that the batch's input is the same tensor value
+  (``torch.equal``; a dataset with random transforms recomputes).
 * Elsewhere (host-resident model, or a model with buffers such as BatchNorm,
   whose running statistics cannot be updated under vmap) the teachers run one
   after another, as in the reference, and their logits go through the
@@ -39,6 +53,8 @@ MI355X-first differences (same results):
   equal to it (tests/test_gpu_roundloop.py).
 """
 from __future__ import annotations
+
+import warnings
 
 import torch
 from torch.func import functional_call
@@ -100,11 +116,41 @@ class TeacherEnsemble(object):
         self.batched = (self.slab.device.type == "cuda"
                         and len(list(model.buffers())) == 0)
         self._w32 = None
-        # the traced forward with the Linear layers on the matrix cores
+        self.fallbacks = 0
+        self.fallback_reason = None
+        self.program = None
+        # the traced forward with its layers on the matrix cores
         # (teacher_program.py); checked against the vmap path on first use
-        self.program = teacher_program.build(model, self.named, self.slab) \
-            if (program and self.batched) else None
+        if program and self.batched:
+            self.program, why = teacher_program.build_or_reason(model, self.named, self.slab)
+            if self.program is None:
+                self._fall_back(why)
         self._checked = False
+
+    def _fall_back(self, reason: str) -> None:
+        """The replay (or the batched path) is not used: count it, warn once."""
+        self.fallbacks += 1
+        self.fallback_reason = reason
+        warnings.warn(f"FedDF teacher replay not used, {reason}; the teachers run under "
+                      f"{'torch.vmap' if self.batched else 'a per-teacher loop'}",
+                      RuntimeWarning, stacklevel=3)
+
+    @property
+    def deterministic(self) -> bool:
+        """Whether the teachers' outputs are a pure function of the input on
+        the path in use (no random op in the traced graph; a vmap'd forward
+        with one raises, and the per-teacher loop is not trusted)."""
+        if not self.batched:
+            return False
+        return self.program is None or not self.program.has_random_ops
+
+    def stats(self) -> dict:
+        p = self.program
+        return dict(replayed=p is not None, batched=self.batched, fallbacks=self.fallbacks,
+                    reason=self.fallback_reason,
+                    linear_launches=p.linear_launches if p else 0,
+                    conv_launches=p.conv_launches if p else 0,
+                    pool_launches=p.pool_launches if p else 0)
 
     def _forward(self, flat, x):
         return functional_call(self.model, vector_to_named_parameters_like(flat, self.named), (x,))
@@ -127,25 +173,40 @@ class TeacherEnsemble(object):
         ref = self._vmap_logits(x)
         try:
             got = self.program(x)
-            ok = (got.shape == ref.shape and bool(torch.isfinite(got).all() == torch.isfinite(ref).all())
-                  and float(torch.linalg.vector_norm((got - ref).double().nan_to_num())) <=
-                  1e-4 * float(torch.linalg.vector_norm(ref.double().nan_to_num())) + 1e-30)
-        except Exception:  # noqa: BLE001 - a graph the replay cannot run: keep vmap
-            got, ok = None, False
+            err = float(torch.linalg.vector_norm((got - ref).double().nan_to_num())) \
+                if got.shape == ref.shape else float("inf")
+            bound = 1e-4 * float(torch.linalg.vector_norm(ref.double().nan_to_num())) + 1e-30
+            ok = (err <= bound
+                  and bool(torch.isfinite(got).all() == torch.isfinite(ref).all()))
+            why = None if ok else (
+                f"its first batch differs from the vmap'd forward (normwise {err / bound * 1e-4:.3g}"
+                f" > 1e-4)" if got.shape == ref.shape else
+                f"its output shape {tuple(got.shape)} is not {tuple(ref.shape)}")
+        except Exception as e:  # noqa: BLE001 - a graph the replay cannot run: keep vmap
+            got, ok, why = None, False, f"the replay raised {type(e).__name__}: {e}"
         self._checked = True
         if not ok:
             self.program = None
+            self._fall_back(why)
             return ref
         return got
+
+    def _sequential_mean(self, x):
+        agg = SerialAggregator()
+        for k in range(self.K):
+            agg.add("target", self._forward(self.slab[k], x).clone(), 1)
+        return agg.get("target")
 
     @torch.no_grad()
     def mean_logits(self, x):
         if not self.batched:
-            agg = SerialAggregator()
-            for k in range(self.K):
-                agg.add("target", self._forward(self.slab[k], x).clone(), 1)
-            return agg.get("target")
-        logits = self.teacher_logits(x)
+            return self._sequential_mean(x)
+        try:
+            logits = self.teacher_logits(x)
+        except Exception as e:  # noqa: BLE001 - e.g. random ops under vmap
+            self.batched, self.program = False, None
+            self._fall_back(f"the vmap'd forward raised {type(e).__name__}: {e}")
+            return self._sequential_mean(x)
         K, shape = logits.shape[0], logits.shape[1:]
         rows = logits.reshape(K, -1).float().contiguous()
         if self._w32 is None:
@@ -195,18 +256,24 @@ class FedDF(FedAvg):
             teachers = TeacherEnsemble(model, appendix_aggregator.get_values("local_params"),
                                        device)
             # the same batches every epoch: mean logits computed once, reused
+            # for a batch whose input is the same value again
             cache = [] if (global_epochs > 1 and _in_order(train_data_loader)
                            and _pure_forward(model)) else None
             ran = False
             for _ in range(global_epochs):
                 for j, (x, _) in enumerate(train_data_loader):
                     x = x.to(device)
-                    if cache is not None and j < len(cache):
-                        logits = cache[j]
+                    if cache is not None and not teachers.deterministic:
+                        cache = None
+                    if cache is not None and j < len(cache) and torch.equal(cache[j][0], x):
+                        logits = cache[j][1]
                     else:
                         logits = teachers.mean_logits(x)
                         if cache is not None:
-                            cache.append(logits)
+                            if j < len(cache):
+                                cache[j] = (x, logits)
+                            else:
+                                cache.append((x, logits))
                     target_out = log_softmax(logits, 1)
                     criterion = KLDivScore(log_target=True)
                     param_dict = vector_to_named_parameters_like(cloud_params,
@@ -222,4 +289,5 @@ class FedDF(FedAvg):
                     ran = True
             if ran:
                 teachers.load_last()
+            server_storage.write("teacher_replay", teachers.stats())
         return serial_aggregator.pop_all()

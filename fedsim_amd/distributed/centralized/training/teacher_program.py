@@ -23,13 +23,19 @@ slab of their flat vectors (parameters_to_vector layout):
   A conv or pool node whose runtime shapes the kernels do not take runs the
   same way.
 
-``build`` returns None when the model does not trace, so the caller keeps
-its whole-model ``vmap`` path; the ensemble also checks the replay against
-that path on its first batch before using it (feddf.py TeacherEnsemble).
+A parameterless module from outside ``torch.nn`` (torchvision's ``Resize``
+at the head of every reference model, simple_models.py:47,107,195, whose
+forward branches on the input's shape) is traced as one leaf call rather than
+into; on the input it runs once per batch, unbatched.
+
+``build`` returns None when the model does not trace (``build_or_reason``
+also says why), so the caller keeps its whole-model ``vmap`` path; the
+ensemble also checks the replay against that path on its first batch before
+using it, and counts and reports every fallback (feddf.py TeacherEnsemble).
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 from torch import nn
@@ -40,6 +46,32 @@ from .... import ops
 
 F = torch.nn.functional
 _RELU_FUNCS = (torch.relu, F.relu)
+# graph nodes whose value is random: a forward that has one is not a pure
+# function of (teacher, input), so its outputs may not be reused
+_RANDOM_FUNCS = {F.dropout, F.dropout1d, F.dropout2d, F.dropout3d, F.alpha_dropout,
+                 F.feature_alpha_dropout, torch.dropout, torch.rand, torch.randn,
+                 torch.rand_like, torch.randn_like, torch.randint, torch.randint_like,
+                 torch.randperm, torch.bernoulli, torch.normal, torch.multinomial,
+                 torch.poisson}
+_RANDOM_METHODS = {"normal_", "uniform_", "bernoulli_", "random_", "exponential_",
+                   "geometric_", "log_normal_", "cauchy_"}
+
+
+class _Tracer(torch.fx.Tracer):
+    """torch.fx's default tracer, except that a module with no parameters
+    and no buffers from outside ``torch.nn`` is one leaf call."""
+
+    def is_leaf_module(self, m: nn.Module, qualname: str) -> bool:
+        if super().is_leaf_module(m, qualname):
+            return True
+        return (not type(m).__module__.startswith("torch.")
+                and next(m.parameters(), None) is None and next(m.buffers(), None) is None)
+
+
+def _trace(model: nn.Module) -> torch.fx.GraphModule:
+    tracer = _Tracer()
+    graph = tracer.trace(model)
+    return torch.fx.GraphModule(tracer.root, graph, type(model).__name__)
 
 
 def _bind(node, names, defaults):
@@ -162,7 +194,7 @@ class TeacherProgram(object):
         # teacher_conv2d / pad_lrn_maxpool, same signatures), so the graph
         # replay can be checked on the CPU
         self.impl = ops if impl is None else impl
-        self.gm = torch.fx.symbolic_trace(model)
+        self.gm = _trace(model)
         self.modules = dict(self.gm.named_modules())
         self.slab = slab
         self.K = slab.shape[0]
@@ -188,6 +220,18 @@ class TeacherProgram(object):
         self.linear_launches = 0
         self.conv_launches = 0
         self.pool_launches = 0
+
+    @property
+    def has_random_ops(self) -> bool:
+        """Whether the traced forward draws random numbers (dropout, rand ...),
+        outside of leaf modules (train-mode ``nn.Dropout`` modules are the
+        caller's check, feddf._pure_forward)."""
+        for node in self.gm.graph.nodes:
+            if node.op == "call_function" and node.target in _RANDOM_FUNCS:
+                return True
+            if node.op == "call_method" and node.target in _RANDOM_METHODS:
+                return True
+        return False
 
     def _is_linear(self, node) -> bool:
         return (node.op == "call_module" and type(self.modules.get(node.target)) is nn.Linear
@@ -411,14 +455,20 @@ class TeacherProgram(object):
         return v
 
 
-def build(model: nn.Module, named, slab: torch.Tensor, impl=None) -> Optional[TeacherProgram]:
-    """A TeacherProgram for ``model``, or None when its forward does not trace,
+def build_or_reason(model: nn.Module, named, slab: torch.Tensor,
+                    impl=None) -> Tuple[Optional[TeacherProgram], Optional[str]]:
+    """(TeacherProgram, None), or (None, why not): its forward does not trace,
     uses parameters outside its own ``named_parameters`` layout, or has no
     Linear / Conv2d layer for the matrix cores to run."""
     try:
         prog = TeacherProgram(model, named, slab, impl)
-    except Exception:  # noqa: BLE001 - untraceable forward: the caller keeps vmap
-        return None
+    except Exception as e:  # noqa: BLE001 - untraceable forward: the caller keeps vmap
+        return None, f"the forward does not trace ({type(e).__name__}: {e})"
     if not any(s.kind in ("linear", "conv") for s in prog.segments):
-        return None
-    return prog
+        return None, "the forward has no nn.Linear / nn.Conv2d layer to replay"
+    return prog, None
+
+
+def build(model: nn.Module, named, slab: torch.Tensor, impl=None) -> Optional[TeacherProgram]:
+    """A TeacherProgram for ``model``, or None (see ``build_or_reason``)."""
+    return build_or_reason(model, named, slab, impl)[0]

@@ -107,8 +107,14 @@ def _handed_over(t: torch.Tensor) -> bool:
         return False
     if _refcount(t) > _OWNED_REFS:
         return False
-    if isinstance(t, SlabRow):  # a reserved slab row: no storage of its own
-        return True
+    if isinstance(t, SlabRow):
+        if t.in_slab:  # a reserved slab row: no storage of its own
+            return True
+        # read back already: torch ops on it may have handed out views of
+        # its copy, which add would then borrow
+        t = t._dense
+        if t is None:
+            return False
     # one TensorImpl + the temporary storage object created here
     return torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= 2
 

@@ -511,23 +511,39 @@ class SerialAggregator(object):
         or None if this key cannot take one (not part of the reference API).
         The key does not exist for ``in`` / ``pop_all`` until a value is
         added."""
+        dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
         e = self._members.get(key)
         if e is None:
             e = self._reserved.get(key)
+            if e is not None and (e.P != P or e.dev != dev):
+                # a reservation for another size / device that was never
+                # added: drop it (live rows keep a copy) and start over
+                e.release()
+                del self._reserved[key]
+                e = None
         if e is None:
-            like = _Like((P,), torch.device(device))
+            like = _Like((P,), dev)
             e = _DeviceEntry(like, _hip_device(like, self._opts.device), self._opts, self)
+            if e.dev != dev:
+                return None
             self._reserved[key] = e
-        if type(e) is not _DeviceEntry or e.P != P or e.dev != torch.device(device) \
-                or e.shape != (P,):
+        if type(e) is not _DeviceEntry or e.P != P or e.dev != dev or e.shape != (P,):
             return None
         return e.reserve()
 
     def add(self, key, value, weight=None):
         entry = self._members.get(key)
         if entry is None and key in self._reserved and self._is_device_value(value):
-            entry = self._members[key] = self._reserved.pop(key)
-            entry.out_device = value.device  # results go where the first value came from
+            res = self._reserved.pop(key)
+            if tuple(value.shape) == res.shape:
+                # the first add defines the key, as in the reference: adopt
+                # the reserved ring only for a value of its shape
+                entry = self._members[key] = res
+                entry.out_device = value.device  # results go where the first value came from
+            else:
+                res.release()  # a reserved row still alive keeps a copy
         if isinstance(entry, _TensorEntry):
             if not self._is_device_value(value):
                 raise TypeError(f"key {key!r} aggregates tensors; got {type(value).__name__}")

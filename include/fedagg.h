@@ -56,7 +56,10 @@
 extern "C" {
 #endif
 
-#define FEDAGG_ABI_VERSION 1
+/* 1: round-1 reduce / pack / step entry points; 2: + the FedDF teacher
+   (linear, conv2d, pad-LRN-maxpool) and slab-row (pack_segments, unpack_row)
+   entry points and their structs */
+#define FEDAGG_ABI_VERSION 2
 
 /* flags for the reduce entry points */
 #define FEDAGG_INIT      0x1  /* ignore acc_in: start from +0.0f (first batch of a round) */

@@ -113,3 +113,22 @@ def host_signature():
     except OSError:
         pass
     return f"{model} | {torch.backends.cpu.get_cpu_capability()}"
+
+
+class ImageDataManager(FakeDataManager):
+    """FakeDataManager whose server split holds image batches, for FedDF
+    rounds on the reference's CNNs (SimpleCNN: 1 x 28 x 28, 10 classes;
+    SimpleCNN2: 3 x 24 x 24, 100 classes).  Client splits are index lists:
+    only their length (num_samples) is read by the synthetic client."""
+
+    def __init__(self, num_clients, image_shape, num_classes, valid_size):
+        super().__init__(num_clients)
+        self.image_shape = tuple(image_shape)
+        self.num_classes = num_classes
+        self.valid_size = valid_size
+
+    def get_global_dataset(self):
+        n, shape = self.valid_size, self.image_shape
+        x = V.gauss(90101, n * int(np.prod(shape))).astype(np.float32).reshape(n, *shape)
+        y = V.randint(90102, n, 0, self.num_classes - 1)
+        return {"valid": TensorDataset(torch.from_numpy(x), torch.from_numpy(y))}

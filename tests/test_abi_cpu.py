@@ -285,3 +285,19 @@ def test_struct_layouts_match_the_header(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(py), cname
         for field, _ in py._fields_:
             assert got[(cname, field)] == getattr(py, field).offset, (cname, field)
+
+
+def test_stale_library_fails_with_the_version_message(tmp_path, monkeypatch):
+    """A libfedagg.so built against an older header (ABI 1: before the
+    FedDF / slab-row entry points) is refused with the version message before
+    any symbol lookup, rather than failing on the first missing entry point."""
+    from fedsim_amd import _native
+
+    src = tmp_path / "old.c"
+    src.write_text("int fedagg_abi_version(void) { return 1; }\n")
+    so = tmp_path / "libfedagg_old.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
+    monkeypatch.setattr(_native, "LIB_PATH", str(so))
+    monkeypatch.setattr(_native, "_lib", None)
+    with pytest.raises(_native.FedAggError, match="ABI version 1, this package needs 2"):
+        _native.load()

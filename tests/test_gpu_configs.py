@@ -12,17 +12,37 @@ last 64 (the ragged column block) -- and through size-independent properties.
       order; and the client-sharded (reordered) decomposition of the same
       clients over 8 virtual ranks: normwise <= 1e-6 vs the in-order result
       and the gamma_K forward-error bound vs fp64 on the sampled columns
+  (d) configs 1-3 at the CLI's default participation (-c 0.01): config 1
+      (FedAvg, SimpleMLP, 500 clients -> K=5, pageable host client vectors,
+      cloud on the host, as ``fed-learn --device cpu`` runs it) and configs 2
+      and 3 (FedAvg / AdaBest mu 0.01 beta 0.6, SimpleCNN2(num_classes=100),
+      1000 clients -> K=10, host and HBM) through CentralFLAlgorithm for 3
+      rounds: bitwise the reference's own round loop (tests/golden/
+      configs.json, tools/gen_golden_configs.py)
+  (e) configs 2 and 3 at full participation (-c 1.0): 1000 GPU clients of
+      SimpleCNN2's size (1 085 668) writing their vectors into the round's
+      slab rows (the production client path, local_updates.sgd_update),
+      through CentralFLAlgorithm -> FedAvg.optimize / AdaBest.optimize (the
+      split pop + server step that ops.fuse_step_pays picks at this size):
+      bitwise against the oracle on 4 096 + 128 sampled columns
 
 Reference arithmetic: SerialAggregator.add / pop (fedsim/utils/aggregators.py
 :17-40, 104-122), FedAvg.optimize (training/fedavg.py:193-208), AdaBest.optimize
 (training/adabest.py:172-189).
 """
+import json
+import os
+import random
+from functools import partial
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import bits
+from conftest import GOLDEN_DIR, bits
 from oracle import ref
+from oracle import synthetic_fl as S
+from oracle import vectors as V
 
 pytestmark = pytest.mark.gpu
 
@@ -214,3 +234,117 @@ def test_config5_streamed_pool_and_reordered_decomposition():
     got = reord[c].cpu().numpy().astype(np.float64)
     assert np.all(np.abs(got - y64) <= bound)
 
+
+
+with open(os.path.join(GOLDEN_DIR, "configs.json")) as _f:
+    _CFG = json.load(_f)
+
+
+@pytest.mark.parametrize("device", ["cpu", "cuda"])
+@pytest.mark.parametrize("rid", [r["id"] for r in _CFG["runs"]])
+def test_configs_1_to_3_cli_defaults_bitwise_vs_reference_round_loop(rid, device):
+    """(d) The reference's own 3-round trajectory of the config at the CLI's
+    default participation, bit for bit: device="cpu" gives pageable host
+    client vectors and a host cloud (the ingest path), device="cuda" HBM
+    ones (borrowed rows)."""
+    from fedsim_amd import models
+    from fedsim_amd.distributed.centralized import training
+
+    run = [r for r in _CFG["runs"] if r["id"] == rid][0]
+    cls = S.make_algorithm(getattr(training, run["algorithm"]))
+    random.seed(S.RANDOM_SEED)
+    torch.manual_seed(S.TORCH_SEED)
+    alg = cls(data_manager=S.FakeDataManager(run["num_clients"]), metric_logger=None,
+              num_clients=run["num_clients"], sample_scheme="uniform",
+              sample_rate=run["sample_rate"],
+              model_def=partial(getattr(models, run["model"]), **run["model_kwargs"]), epochs=1,
+              criterion_def="CrossEntropyScore", optimizer_def=partial(torch.optim.SGD, lr=1.0),
+              device=device, **run["alg_kwargs"])
+    scores = alg.train(rounds=_CFG["rounds"])
+    st = alg.get_server_storage()
+    cloud = st.read("cloud_params")
+    assert cloud.device.type == device and cloud.numel() == run["P"]
+    assert V.sha256(cloud.detach().cpu().numpy()) == run["cloud_sha256"]
+    if "avg_params_sha256" in run:
+        assert V.sha256(st.read("avg_params").detach().cpu().numpy()) == run["avg_params_sha256"]
+    assert {k: float(v) for k, v in scores.items()} == run["scores"]
+
+
+def _gpu_slab_client(record, cols):
+    """A client that trains on the GPU, as local_updates.sgd_update hands its
+    update over: its model's parameters become views of one fresh device
+    vector (cloud + a seeded N(0, 1e-3) delta), which vectorize_module packs
+    into the round's reserved slab row.  Records (vector[cols], weight)."""
+    from torch.nn.utils import parameters_to_vector, vector_to_parameters
+
+    from fedsim_amd.utils import vectorize_module
+    from fedsim_amd.utils.slab_rows import reserve_round_row
+
+    def send_to_server(id, rounds, storage, datasets, train_split_name, scores, epochs,
+                       criterion, train_batch_size, inference_batch_size, optimizer_def,
+                       lr_scheduler_def=None, device="cuda", ctx=None, step_closure=None):
+        model = ctx["model"]
+        base = parameters_to_vector(model.parameters()).detach()
+        g = torch.Generator(device=base.device).manual_seed(1_000_003 * rounds + id)
+        local = base + torch.empty_like(base).normal_(0.0, 1e-3, generator=g)
+        vector_to_parameters(local, model.parameters())
+        row = reserve_round_row("local_params", model)
+        assert row is not None and row.in_slab
+        n = len(datasets[train_split_name])
+        record.append((local[cols], n))
+        return dict(local_params=vectorize_module(model, out=row), num_steps=max(1, n // 32),
+                    diverged=False, num_samples={train_split_name: n},
+                    metrics={train_split_name: {"loss": 1.0 + 0.001 * id}})
+
+    return send_to_server
+
+
+@pytest.mark.parametrize("algo", ["FedAvg", "AdaBest"])
+def test_configs_2_3_full_participation_slab_rows_1000x1_085_668(algo):
+    """(e) -c 1.0: K = 1000 clients x SimpleCNN2's 1 085 668 parameters, one
+    round through the round driver with every client in a slab row; the
+    server step is the split pass at this size."""
+    from fedsim_amd import models, ops
+    from fedsim_amd.distributed.centralized import training
+
+    _need(10)
+    n_clients, P = 1000, 1_085_668
+    cols = _sample_cols(P)
+    c = torch.from_numpy(cols).to(DEV)
+    record = []
+    base = getattr(training, algo)
+    cls = type("Gpu" + algo, (base,), {"send_to_server": _gpu_slab_client(record, c)})
+    akw = dict(mu=0.01, beta=0.6) if algo == "AdaBest" else {}
+    random.seed(S.RANDOM_SEED)
+    torch.manual_seed(S.TORCH_SEED)
+    alg = cls(data_manager=S.FakeDataManager(n_clients), metric_logger=None,
+              num_clients=n_clients, sample_scheme="uniform", sample_rate=1.0,
+              model_def=partial(models.SimpleCNN2, num_classes=100), epochs=1,
+              criterion_def="CrossEntropyScore", optimizer_def=partial(torch.optim.SGD, lr=1.0),
+              device="cuda", **akw)
+    st = alg.get_server_storage()
+    cloud0 = st.read("cloud_params").detach()[c].cpu().numpy()
+    prev0 = st.read("avg_params")[c].cpu().numpy() if algo == "AdaBest" else None
+    assert st.read("cloud_params").numel() == P
+    split = []
+    orig = ops.fuse_step_pays
+    ops.fuse_step_pays = lambda *a, **k: split.append(not orig(*a, **k)) or orig(*a, **k)
+    try:
+        alg.train(rounds=0)  # one round
+    finally:
+        ops.fuse_step_pays = orig
+    assert len(record) == n_clients
+    assert split and all(split)  # the split pop + step at this size
+    sub = torch.stack([v for v, _ in record]).cpu().numpy()  # [K, n] in arrival order
+    w = [n for _, n in record] if algo == "FedAvg" else [1] * n_clients
+    avg = ref.reduce(sub, w, W=sum(w))
+    if algo == "FedAvg":
+        state = ref.ServerState("fedavg", cloud0, dict(lr=1.0))
+    else:
+        state = ref.ServerState("adabest", cloud0, dict(lr=1.0), aux=prev0, coef=0.6)
+    state.step(avg)
+    cloud = st.read("cloud_params").detach()
+    np.testing.assert_array_equal(bits(cloud[c].cpu().numpy()), bits(state.cloud))
+    if algo == "AdaBest":
+        np.testing.assert_array_equal(bits(st.read("avg_params")[c].cpu().numpy()), bits(avg))
+    assert torch.isfinite(cloud).all()

@@ -237,3 +237,83 @@ def test_replay_in_teacher_chunks():
     assert prog.K == K and prog.slab is slab
     assert prog.conv_launches == 2 * 3  # two convs x three passes (3, 3, 1 teachers)
     torch.testing.assert_close(got, whole, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("name,kw,shape", [
+    ("SimpleMLP", {}, (3, 1, 28, 28)),
+    ("SimpleCNN", {}, (3, 1, 28, 28)),
+    ("SimpleCNN2", dict(num_classes=100), (3, 3, 24, 24)),
+])
+def test_reference_models_replay_with_their_resize_leaf(name, kw, shape):
+    """The reference's own model classes (fedsim_amd/models.py restates
+    simple_models.py:23-256) start with a parameterless Resize whose forward
+    branches on the input shape, as torchvision's does: the replay keeps it
+    as one unbatched leaf call and still puts every Linear / Conv2d layer and
+    pool chain on the kernels (a CLI run with ``model_def=SimpleCNN2`` does
+    not drop to the whole-model vmap)."""
+    from fedsim_amd import models
+
+    torch.manual_seed(1)
+    model = getattr(models, name)(**kw)
+    named = list(model.named_parameters())
+    K = 3
+    base = torch.cat([p.detach().reshape(-1) for _, p in named])
+    slab = torch.stack([base + 0.01 * torch.randn_like(base) for _ in range(K)])
+    with pytest.raises(Exception):  # plain fx cannot trace through the resize
+        torch.fx.symbolic_trace(model)
+    prog, why = TP.build_or_reason(model, named, slab, impl=STUBS)
+    assert prog is not None, why
+    leaves = [n for n in prog.gm.graph.nodes if n.op == "call_module" and n.target == "resize"]
+    assert len(leaves) == 1
+    x = torch.randn(*shape)
+    got = prog(x)
+    want = torch.stack([functional_call(model, vector_to_named_parameters_like(slab[k], named),
+                                        (x,)) for k in range(K)])
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+    n_conv = sum(isinstance(m, nn.Conv2d) for m in model.modules())
+    assert prog.linear_launches == sum(isinstance(m, nn.Linear) for m in model.modules())
+    assert prog.conv_launches == n_conv and prog.pool_launches == n_conv
+    assert not prog.has_random_ops
+
+
+def test_untraceable_model_reports_why():
+    class Dyn(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.l = nn.Linear(3, 2)
+
+        def forward(self, x):
+            if x.sum() > 0:
+                return self.l(x)
+            return -self.l(x)
+
+    m = Dyn()
+    slab = torch.zeros(2, sum(p.numel() for p in m.parameters()))
+    prog, why = TP.build_or_reason(m, list(m.named_parameters()), slab, impl=STUBS)
+    assert prog is None and "does not trace" in why
+
+
+def test_random_ops_in_the_graph_are_detected():
+    """Functional dropout / random draws make a teacher's output impure: FedDF
+    must not reuse its targets across epochs (feddf.TeacherEnsemble)."""
+    class Drop(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.l = nn.Linear(4, 3)
+
+        def forward(self, x):
+            return torch.nn.functional.dropout(self.l(x), 0.3, training=True)
+
+    class Noise(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.l = nn.Linear(4, 3)
+
+        def forward(self, x):
+            return self.l(x + torch.randn_like(x))
+
+    for cls, random in ((Drop, True), (Noise, True), (Tiny, False)):
+        m = cls()
+        slab = torch.zeros(2, sum(p.numel() for p in m.parameters()))
+        prog = TP.build(m, list(m.named_parameters()), slab, impl=STUBS)
+        assert prog is not None and prog.has_random_ops is random, cls
