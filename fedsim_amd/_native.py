@@ -38,6 +38,8 @@ FEDAGG_FAST = 0x200000
 FEDAGG_RELU = 0x400000
 FEDAGG_CONV_GATHER = 0x800000
 FEDAGG_POOL_PLANES = 0x1000000
+FEDAGG_CONV_MAXPOOL2 = 0x2000000
+FEDAGG_CONV_POOL_PAD1 = 0x4000000
 FEDAGG_EINVAL = -22
 
 FEDAGG_ALGO_FEDAVG = 0
@@ -151,6 +153,7 @@ SIGNATURES = {
     ),
     "fedagg_conv_stage": (ctypes.c_int, [ctypes.c_int64]),
     "fedagg_conv_order": (ctypes.c_int, [ctypes.POINTER(Conv2dShape), ctypes.c_int]),
+    "fedagg_conv_pool_fusable": (ctypes.c_int, [ctypes.POINTER(Conv2dShape), ctypes.c_int]),
     "fedagg_pool_output": (
         ctypes.c_int,
         [ctypes.POINTER(PoolArgs), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),

@@ -1596,6 +1596,37 @@ __global__ __launch_bounds__(256) void k_teacher_linear(
 // before this stage's MFMAs.  Exact f32: each output is the r-ordered fmaf
 // chain (zero-filled tail to a multiple of RK), then the bias, then ReLU.
 // ---------------------------------------------------------------------------
+// XCD-aware tile order for the teacher convolutions.  The hardware deals
+// consecutive workgroups of a launch round-robin over the 8 XCDs (blocks b
+// and b + 8 share one; MI355X_MICROARCH.md, workgroup dispatch), so in the
+// plain (pixel tile, channel tile, teacher) order every teacher's tiles are
+// spread over all 8 XCDs and its weights, and the images two neighbouring
+// pixel tiles share, are fetched into up to eight L2s.  Renumbered, each
+// XCD walks one contiguous range of the tile order: a teacher's weights are
+// read from HBM about once, and the partial cache lines two neighbouring
+// tiles write at an image boundary merge in one L2.  Bijective for any grid;
+// placement only changes speed, never results.
+#ifndef FEDAGG_CONV_XCD_ORDER  // 0: plain dispatch order (A/B builds)
+#define FEDAGG_CONV_XCD_ORDER 1
+#endif
+struct ConvTile {
+  int x, y, z;
+};
+__device__ __forceinline__ ConvTile conv_tile_order() {
+  const uint32_t gx = gridDim.x, gy = gridDim.y;
+  if (!FEDAGG_CONV_XCD_ORDER) return {int(blockIdx.x), int(blockIdx.y), int(blockIdx.z)};
+  const uint32_t gxy = gx * gy, n = gxy * gridDim.z;
+  const uint32_t L = blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z;
+  const uint32_t xcd = L & 7u, slot = L >> 3, q = n >> 3, r = n & 7u;
+  const uint32_t lg = slot + (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q);
+  const uint32_t z = lg / gxy, rem = lg - z * gxy;
+  const uint32_t y = rem / gx;
+  // wave-uniform by construction; readfirstlane keeps the tile coordinates
+  // (and the buffer descriptors built from them) in SGPRs
+  return {__builtin_amdgcn_readfirstlane(int(rem - y * gx)), __builtin_amdgcn_readfirstlane(int(y)),
+          __builtin_amdgcn_readfirstlane(int(z))};
+}
+
 constexpr int kTC_OC = 64;    // output channels per workgroup
 constexpr int kTC_PX = 256;   // output pixels per workgroup (64 per wave)
 constexpr int kTC_WPAD = 1;   // sW row pad: 32 lanes reading 32 rows hit 32 banks
@@ -1612,9 +1643,10 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
   // from SGPRs, so the buffer resources below are wave-uniform (a descriptor
   // derived from a VALU division makes the compiler wrap every load in a
   // waterfall loop)
-  const int64_t k = blockIdx.z;
-  const int64_t oc0 = int64_t(blockIdx.y) * kTC_OC;
-  const int64_t px0 = int64_t(blockIdx.x) * kTC_PX;
+  const ConvTile tile = conv_tile_order();
+  const int64_t k = tile.z;
+  const int64_t oc0 = int64_t(tile.y) * kTC_OC;
+  const int64_t px0 = int64_t(tile.x) * kTC_PX;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
@@ -1779,9 +1811,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_LDS_
   // grid (pixel tiles, channel tiles, teachers): tile coordinates straight
   // from the SGPRs, so the buffer descriptors below are provably uniform (one
   // derived from a VALU division costs a waterfall loop per load)
-  const int64_t k = blockIdx.z;
-  const int oc0 = blockIdx.y * kTC_OC;
-  const int pxt = blockIdx.x;
+  const ConvTile tile = conv_tile_order();
+  const int64_t k = tile.z;
+  const int oc0 = tile.y * kTC_OC;
+  const int pxt = tile.x;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
@@ -1968,11 +2001,31 @@ constexpr int kFlatThreads = 64 * FEDAGG_FLAT_WAVES;
 #ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds;
 #define FEDAGG_FLAT_WPE 4  // 4: SimpleCNN2 conv1 2.26 ms vs 2.52 ms with 3, profiles/r02x3)
 #endif
-template <int KS, int CI, int XM, bool HALF>
+// POOL: the 2 x 2 / stride 2 max pool (padding ppad = 0 or 1) that follows
+// the layer is fused into the store (FEDAGG_CONV_MAXPOOL2; SimpleCNN's
+// relu -> max_pool2d(2, 2, padding=1), simple_models.py:156-159).  The
+// tile's pixel slots then run over (image, pooled row, pooled column, window
+// member) with the member fastest, so the four conv outputs of one window
+// sit in one quad of lanes (the MFMA result's pixel dimension is the lane):
+// two DPP quad swaps combine them in window order with max_pool2d's rule
+// (take v if v > m or v is NaN; members in the padding are -inf), and one
+// lane per quad stores the pooled value.  The conv values are the unfused
+// kernel's bits, so the result is the conv + pool pass bit for bit; only
+// the pooled [OC, PH, PW] planes are written.
+template <int CTRL>
+__device__ __forceinline__ float pool_dpp_max(float m) {
+  // m combined with the value of the quad partner selected by CTRL (a LATER
+  // window member for the lanes whose result is used)
+  const float v = __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, m), CTRL, 0xF, 0xF, false));
+  return (v > m || __builtin_isnan(v)) ? v : m;
+}
+
+template <int KS, int CI, int XM, bool HALF, bool POOL>
 __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
-    float* __restrict__ y, int relu) {
+    float* __restrict__ y, int relu, int ppad) {
   constexpr int TAPS = KS * KS;
   constexpr int R = CI * TAPS;
   constexpr int RP = (R + 1) / 2;    // k steps
@@ -1986,9 +2039,10 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   extern __shared__ float lds[];
   float* sW = lds;
   float* sX = lds + kTC_OC * RW;
-  const int64_t k = blockIdx.z;
-  const int oc0 = blockIdx.y * kTC_OC;
-  const int pxt = blockIdx.x;
+  const ConvTile tile = conv_tile_order();
+  const int64_t k = tile.z;
+  const int oc0 = tile.y * kTC_OC;
+  const int pxt = tile.x;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
@@ -1997,10 +2051,16 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int OHW = static_cast<int>(s.OH * s.OW);
   const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = OW + KS - 1, HpWp = Hp * Wp;
   const int HW = H * W;
-  const int NPX = static_cast<int>(s.M) * OHW;
+  const int OH = static_cast<int>(s.OH);
+  // pooled planes (POOL): PH x PW windows of 2 x 2, four pixel slots each
+  const int PH = POOL ? (OH + 2 * ppad - 2) / 2 + 1 : 1;
+  const int PW = POOL ? (OW + 2 * ppad - 2) / 2 + 1 : 1;
+  const int PHW = PH * PW;
+  // pixel slots of the launch: conv pixels, or (window, member) pairs
+  const int NPX = static_cast<int>(s.M) * (POOL ? 4 * PHW : OHW);
   const int OC = static_cast<int>(s.OC);
   const int px0 = pxt * TPX;
-  const int m_lo = px0 / OHW;
+  const int m_lo = POOL ? (px0 >> 2) / PHW : px0 / OHW;
   const int pt = static_cast<int>(s.pad_h), pl = static_cast<int>(s.pad_w);
   const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(x + k * x_kstride), static_cast<short>(0),
@@ -2016,9 +2076,11 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   // (a 256-pixel tile needs ~1/3 of the two 24 x 24 images it touches).
   const int xtot = nslot * CI * HW;
   const int pend = (px0 + TPX < NPX ? px0 + TPX : NPX) - 1;
-  const int last = pend / OHW - m_lo;  // slot of the tile's last image
-  const int row_lo = (px0 - m_lo * OHW) / OW;
-  const int row_hi = (pend - (m_lo + last) * OHW) / OW + KS - 1;
+  // slot of the tile's last image; the padded rows its pixels read (POOL:
+  // whole images, a window's rows straddle the tile's first / last row)
+  const int last = (POOL ? (pend >> 2) / PHW : pend / OHW) - m_lo;
+  const int row_lo = POOL ? 0 : (px0 - m_lo * OHW) / OW;
+  const int row_hi = POOL ? Hp - 1 : (pend - (m_lo + last) * OHW) / OW + KS - 1;
   for (int pc = 0; pc < (last + 1) * CI; ++pc) {
     const int slot = pc / CI;
     const int lo = slot == 0 ? row_lo : 0;
@@ -2069,10 +2131,22 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   for (int b = 0; b < NPG; ++b) {
     int p = px0 + wave * 32 * NPG + b * 32 + col;
     p = p < NPX ? p : NPX - 1;
-    const int m = p / OHW;
-    const int ohw = p - m * OHW;
-    const int oh = ohw / OW;
-    const int ow = ohw - oh * OW;
+    int m, oh, ow;
+    if constexpr (POOL) {  // window q, member d: conv pixel (2i - ppad + d/2, 2j - ppad + d%2)
+      const int q = p >> 2, d = p & 3;
+      m = q / PHW;
+      const int ij = q - m * PHW;
+      const int i = ij / PW;
+      oh = 2 * i - ppad + (d >> 1);
+      ow = 2 * (ij - i * PW) - ppad + (d & 1);
+      oh = oh < 0 ? 0 : oh >= OH ? OH - 1 : oh;  // padding members: any pixel (masked)
+      ow = ow < 0 ? 0 : ow >= OW ? OW - 1 : ow;
+    } else {
+      m = p / OHW;
+      const int ohw = p - m * OHW;
+      oh = ohw / OW;
+      ow = ohw - oh * OW;
+    }
     xb[b] = (m - m_lo) * CI * HpWp + oh * Wp + ow;
   }
   f32x16 acc[2][2];
@@ -2113,6 +2187,46 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   }
   // epilogue: each bias value loaded once for both pixel groups
   const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
+  if constexpr (POOL) {
+    // a quad of lanes holds one window's members in order; all four lanes of
+    // a quad are in or out of the launch together (NPX is a multiple of 4)
+    float* yq[NPG];
+    bool pin[NPG], inside[NPG];
+#pragma unroll
+    for (int b = 0; b < NPG; ++b) {
+      const int p = px0 + wave * 32 * NPG + b * 32 + col;
+      pin[b] = p < NPX;
+      const int q = (pin[b] ? p : 0) >> 2, d = p & 3;
+      const int m = q / PHW;
+      const int ij = q - m * PHW;
+      const int i = ij / PW;
+      const int oh = 2 * i - ppad + (d >> 1);
+      const int ow = 2 * (ij - i * PW) - ppad + (d & 1);
+      inside[b] = oh >= 0 && oh < OH && ow >= 0 && ow < OW;
+      yq[b] = y + (k * s.M + m) * s.OC * PHW + ij;
+    }
+    const bool leader = (col & 3) == 0;
+#pragma unroll
+    for (int a = 0; a < (HALF ? 1 : 2); ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
+        if (oc >= OC) continue;  // uniform over each 32-lane half, so over quads
+        const float bias = bk ? bk[oc] : 0.f;
+#pragma unroll
+        for (int b = 0; b < NPG; ++b) {
+          if (!pin[b]) continue;
+          float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias;
+          if (relu) v = v > 0.f ? v : 0.f;
+          if (!inside[b]) v = -__builtin_huge_valf();
+          v = pool_dpp_max<0xB1>(v);  // members (0, 1) and (2, 3): quad_perm [1, 0, 3, 2]
+          v = pool_dpp_max<0x4E>(v);  // then (01, 23): quad_perm [2, 3, 0, 1]
+          if (leader) yq[b][int64_t(oc) * PHW] = v;
+        }
+      }
+    }
+    return;
+  }
   float* yp[NPG];
   bool pin[NPG];
 #pragma unroll
@@ -2149,7 +2263,7 @@ struct ConvLdsPlan {
   size_t lds;
 };
 
-bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
+bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = -1) {
   if (s.KH != s.KW || (s.KH != 5 && s.KH != 3) || s.stride_h != 1 || s.stride_w != 1) return false;
   const int64_t ks = s.KH;
   const int64_t Hp = s.OH + ks - 1, Wp = s.OW + ks - 1;
@@ -2160,7 +2274,12 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
   if (nslot > s.M) nslot = s.M;
   if (s.C == 1 || s.C == 3) {  // every channel staged at once (k_teacher_conv2d_flat)
     const int64_t tpx = (s.OC <= 32 ? 2 : 1) * kFlatThreads;  // HALF tiles: 512 pixels
-    int64_t fslot = (tpx - 2) / OHW + 2;
+    // images a tile touches: tpx pixels, or tpx / 4 pooled windows (POOL)
+    const int64_t per_img = pool_pad >= 0 ? ((s.OH + 2 * pool_pad - 2) / 2 + 1) *
+                                                ((s.OW + 2 * pool_pad - 2) / 2 + 1)
+                                          : OHW;
+    const int64_t per_tile = pool_pad >= 0 ? tpx / 4 : tpx;
+    int64_t fslot = (per_tile - 2) / per_img + 2;
     if (fslot > s.M) fslot = s.M;
     const int64_t xall = s.C * fslot * HW;
     if (xall <= 16 * kFlatThreads) {
@@ -2173,6 +2292,7 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p) {
       if (p->lds <= 64 * 1024) return true;
     }
   }
+  if (pool_pad >= 0) return false;  // the pool is fused by the flat kernel only
 #ifndef FEDAGG_CONV_CC2_XM16  // chunks of 2 channels where 4 would need 16 staging registers
 #define FEDAGG_CONV_CC2_XM16 1  // (SimpleCNN conv2, 32 ch at 14x14: whole teacher batch at
 #endif                          // K=1000 14.55 -> 13.97 ms, profiles/r02xa; 0 for A/B builds)
@@ -2822,6 +2942,23 @@ int fedagg_conv_stage(int64_t R) {
   return ((R + 15) / 16 * 16 < (R + 31) / 32 * 32) ? 16 : 32;
 }
 
+// 2 x 2 / stride 2 max pool padding requested by the conv flags, or -1
+static int conv_pool_pad(int flags) {
+  if (!(flags & FEDAGG_CONV_MAXPOOL2)) return -1;
+  return (flags & FEDAGG_CONV_POOL_PAD1) ? 1 : 0;
+}
+
+int fedagg_conv_pool_fusable(const fedagg_conv2d_shape* shape, int flags) {
+  if (!shape || !(flags & FEDAGG_CONV_MAXPOOL2) || (flags & FEDAGG_CONV_GATHER)) return 0;
+  const fedagg_conv2d_shape& s = *shape;
+  const int pp = conv_pool_pad(flags);
+  if (s.OH + 2 * pp < 2 || s.OW + 2 * pp < 2 || s.M <= 0) return 0;
+  const int64_t PH = (s.OH + 2 * pp - 2) / 2 + 1, PW = (s.OW + 2 * pp - 2) / 2 + 1;
+  if (s.M * PH * PW * 4 >= (int64_t(1) << 31)) return 0;
+  ConvLdsPlan plan;
+  return conv_lds_plan(s, &plan, pp) && plan.cc == 0 ? 1 : 0;
+}
+
 int fedagg_conv_order(const fedagg_conv2d_shape* shape, int flags) {
   ConvLdsPlan plan;
   if (!shape || (flags & FEDAGG_CONV_GATHER) || !conv_lds_plan(*shape, &plan)) return 0;
@@ -2834,7 +2971,10 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
                               void* stream) {
   if (!shape || K < 0 || x_kstride < 0 || params_kstride < 0 || w_off < 0 || b_off < -1)
     return FEDAGG_EINVAL;
-  if (flags & ~(FEDAGG_RELU | FEDAGG_CONV_GATHER)) return FEDAGG_EINVAL;
+  if (flags & ~(FEDAGG_RELU | FEDAGG_CONV_GATHER | FEDAGG_CONV_MAXPOOL2 | FEDAGG_CONV_POOL_PAD1))
+    return FEDAGG_EINVAL;
+  if ((flags & FEDAGG_CONV_POOL_PAD1) && !(flags & FEDAGG_CONV_MAXPOOL2)) return FEDAGG_EINVAL;
+  const int ppad = conv_pool_pad(flags);
   const fedagg_conv2d_shape s = *shape;
   const int64_t lim = int64_t(1) << 15;
   if (s.M < 0 || s.C <= 0 || s.H <= 0 || s.W <= 0 || s.OC <= 0 || s.KH <= 0 || s.KW <= 0 ||
@@ -2850,6 +2990,7 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   // one teacher's input and weight matrix are addressed by 32-bit buffer offsets
   if (s.M * s.C * s.H * s.W >= (int64_t(1) << 29) || s.OC * R >= (int64_t(1) << 29))
     return FEDAGG_EINVAL;
+  if (ppad >= 0 && !fedagg_conv_pool_fusable(&s, flags)) return FEDAGG_EINVAL;
   if (K == 0 || s.M == 0) return 0;
   if (!x || !params || !y) return FEDAGG_EINVAL;
   const int64_t oc_tiles = (s.OC + kTC_OC - 1) / kTC_OC;
@@ -2859,28 +3000,39 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   const int relu = (flags & FEDAGG_RELU) ? 1 : 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   ConvLdsPlan plan;
-  if (!(flags & FEDAGG_CONV_GATHER) && conv_lds_plan(s, &plan)) {
+  if (!(flags & FEDAGG_CONV_GATHER) && conv_lds_plan(s, &plan, ppad)) {
+    // pixel slots per teacher (the pooled output's size when the pool is fused)
+    const int64_t PHW = ppad >= 0 ? ((s.OH + 2 * ppad - 2) / 2 + 1) * ((s.OW + 2 * ppad - 2) / 2 + 1)
+                                  : 0;
+    const int64_t nslots = ppad >= 0 ? s.M * PHW * 4 : s.M * s.OH * s.OW;
+    const int64_t y_kstride = ppad >= 0 ? s.M * s.OC * PHW : s.M * s.OC * s.OH * s.OW;
     for (int64_t k0 = 0; k0 < K; k0 += 65535) {
       const int64_t kn = K - k0 < 65535 ? K - k0 : 65535;
       const dim3 grid(static_cast<unsigned>(px_tiles), static_cast<unsigned>(oc_tiles),
                       static_cast<unsigned>(kn));
       const float* xk = x + k0 * x_kstride;
       const float* pk = params + k0 * params_kstride;
-      float* yk = y + k0 * s.M * s.OC * s.OH * s.OW;
+      float* yk = y + k0 * (ppad >= 0 ? y_kstride : s.M * s.OC * s.OH * s.OW);
 #define FEDAGG_CONV_LDS(KS, CC, XM)                                                          \
   hipLaunchKernelGGL((k_teacher_conv2d_lds<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
 #define FEDAGG_CONV_FLAT(KS, CI, XM)                                                          \
   do {                                                                                        \
-    if (half) FEDAGG_CONV_FLAT_H(KS, CI, XM, true); else FEDAGG_CONV_FLAT_H(KS, CI, XM, false); \
+    if (ppad >= 0) {                                                                          \
+      if (half) FEDAGG_CONV_FLAT_H(KS, CI, XM, true, true);                                   \
+      else FEDAGG_CONV_FLAT_H(KS, CI, XM, false, true);                                       \
+    } else {                                                                                  \
+      if (half) FEDAGG_CONV_FLAT_H(KS, CI, XM, true, false);                                  \
+      else FEDAGG_CONV_FLAT_H(KS, CI, XM, false, false);                                      \
+    }                                                                                         \
   } while (0)
-#define FEDAGG_CONV_FLAT_H(KS, CI, XM, HF)                                                    \
-  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM, HF>), gflat, dim3(kFlatThreads), plan.lds, st, xk, \
-                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
+#define FEDAGG_CONV_FLAT_H(KS, CI, XM, HF, PL)                                                \
+  hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM, HF, PL>), gflat, dim3(kFlatThreads), plan.lds, st, xk, \
+                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu, ppad)
       if (plan.cc == 0) {
         const bool half = s.OC <= 32;
         const int64_t tpx = (half ? 2 : 1) * kFlatThreads;
-        const dim3 gflat(static_cast<unsigned>((s.M * s.OH * s.OW + tpx - 1) / tpx),
+        const dim3 gflat(static_cast<unsigned>((nslots + tpx - 1) / tpx),
                          static_cast<unsigned>(oc_tiles), static_cast<unsigned>(kn));
         if (plan.ks == 5) {
           if (s.C == 3) {

@@ -150,7 +150,8 @@ class TeacherEnsemble(object):
                     reason=self.fallback_reason,
                     linear_launches=p.linear_launches if p else 0,
                     conv_launches=p.conv_launches if p else 0,
-                    pool_launches=p.pool_launches if p else 0)
+                    pool_launches=p.pool_launches if p else 0,
+                    fused_pools=p.fused_pools if p else 0)
 
     def _forward(self, flat, x):
         return functional_call(self.model, vector_to_named_parameters_like(flat, self.named), (x,))

@@ -173,7 +173,7 @@ class _Segment(object):
     Conv2d layer on the matrix cores (kind "linear" / "conv"), or one
     pad / LRN / max-pool chain (kind "pool")."""
 
-    __slots__ = ("kind", "nodes", "inputs", "outputs", "params", "fn", "spec")
+    __slots__ = ("kind", "nodes", "inputs", "outputs", "params", "fn", "spec", "pool_next")
 
     def __init__(self, kind, nodes, spec=None):
         self.kind = kind
@@ -184,6 +184,7 @@ class _Segment(object):
         self.fn = None           # the run as generated code (kind "ops"; the
         #                          fallback of "conv" / "pool")
         self.spec = spec         # conv geometry / pool chain
+        self.pool_next = None    # conv: the 2 x 2 / 2 max-pool segment its store may fuse
 
 
 class TeacherProgram(object):
@@ -220,6 +221,7 @@ class TeacherProgram(object):
         self.linear_launches = 0
         self.conv_launches = 0
         self.pool_launches = 0
+        self.fused_pools = 0  # pool segments run inside the conv's store
 
     @property
     def has_random_ops(self) -> bool:
@@ -321,7 +323,27 @@ class TeacherProgram(object):
         for seg in segs:
             if seg.kind in ("ops", "conv", "pool"):
                 seg.fn = self._compile(seg)
+        for a, b in zip(segs, segs[1:]):
+            if a.kind == "conv" and b.kind == "pool" and self._pool_fusable(a, b):
+                a.pool_next = b
         return segs
+
+    def _pool_fusable(self, conv, pool) -> bool:
+        """A max pool of 2 x 2 / stride 2 (padding 0 or 1; no pad, no LRN)
+        that is the only reader of the conv's (ReLU'd) output: candidates for
+        the conv kernel's pooled store (checked against the runtime shape)."""
+        pads, lrn, spec = pool.spec
+        if pads != (0, 0, 0, 0) or lrn is not None or spec is None:
+            return False
+        kh, kw, sh, sw, ph, pw = spec
+        if (kh, kw, sh, sw) != (2, 2, 2, 2) or ph != pw or ph not in (0, 1):
+            return False
+        node = conv.nodes[0]
+        head = pool.nodes[0]
+        out = [u for u in node.users]
+        if len(out) == 1 and out[0] in self.alias:  # the fused ReLU in between
+            out = list(out[0].users)
+        return out == [head] and pool.inputs == [node]
 
     def _compile(self, seg) -> torch.fx.GraphModule:
         """The run as generated Python (fx codegen): fn(*inputs, *params)
@@ -364,9 +386,12 @@ class TeacherProgram(object):
         self.linear_launches += 1
         return y.view(self.K, *lead, mod.out_features)
 
-    def _conv(self, seg, env) -> bool:
+    def _conv(self, seg, env, done) -> bool:
         """The conv node on the matrix cores; False when its runtime input is
-        not the 4-D (per teacher) f32 image batch the kernel takes."""
+        not the 4-D (per teacher) f32 image batch the kernel takes.  With a
+        fusable max pool after it (SimpleCNN's conv1 -> relu -> max_pool2d(2,
+        2, padding=1)) the pool runs in the conv's store and its segment is
+        added to ``done``."""
         node = seg.nodes[0]
         v, batched = env[seg.inputs[0]]
         if (not isinstance(v, torch.Tensor) or v.dtype != torch.float32
@@ -376,10 +401,22 @@ class TeacherProgram(object):
         kernel, stride, pads = seg.spec
         w = self.offs[node.target + ".weight"][0]
         b = self.offs[node.target + ".bias"][0] if mod.bias is not None else -1
+        pool = None
+        nxt = seg.pool_next
+        fusable = getattr(self.impl, "conv_pool_fusable", None)
+        if nxt is not None and fusable is not None and fusable(
+                v.shape, mod.out_channels, kernel, stride, pads, nxt.spec[2]):
+            pool = nxt.spec[2]
         y = self.impl.teacher_conv2d(v.contiguous(), self.slab, w, b, mod.out_channels, kernel,
-                                     stride, pads, shared=not batched, relu=node in self.fused)
+                                     stride, pads, shared=not batched, relu=node in self.fused,
+                                     pool=pool)
         self.conv_launches += 1
-        env[node] = (y, True)
+        if pool is None:
+            env[node] = (y, True)
+        else:
+            self.fused_pools += 1
+            env[nxt.nodes[-1]] = (y, True)
+            done.add(nxt)
         return True
 
     def _pool(self, seg, env) -> bool:
@@ -437,12 +474,15 @@ class TeacherProgram(object):
 
     def _replay(self, x: torch.Tensor) -> torch.Tensor:
         env = {p: (x, False) for p in self.placeholders}
+        done = set()  # pool segments already run by a conv's pooled store
         for seg in self.segments:
+            if seg in done:
+                continue
             if seg.kind == "linear":
                 node = seg.nodes[0]
                 v, b = env[self.alias.get(node.args[0], node.args[0])]
                 env[node] = (self._linear(node, v, b), True)
-            elif seg.kind == "conv" and self._conv(seg, env):
+            elif seg.kind == "conv" and self._conv(seg, env, done):
                 pass
             elif seg.kind == "pool" and self._pool(seg, env):
                 pass

@@ -436,16 +436,41 @@ def conv_order(x_shape, out_channels: int, kernel_size, stride, padding,
                                                 _native.FEDAGG_CONV_GATHER if gather else 0))
 
 
+def _pool_flags(pool) -> int:
+    """Conv flags fusing ``pool`` = (kh, kw, sh, sw, ph, pw), or -1 when it is
+    not the 2 x 2 / stride 2 pool (padding 0 or 1) the conv kernel fuses."""
+    if pool is None:
+        return 0
+    kh, kw, sh, sw, ph, pw = pool
+    if (kh, kw, sh, sw) != (2, 2, 2, 2) or ph != pw or ph not in (0, 1):
+        return -1
+    return _native.FEDAGG_CONV_MAXPOOL2 | (_native.FEDAGG_CONV_POOL_PAD1 if ph else 0)
+
+
+def conv_pool_fusable(x_shape, out_channels: int, kernel_size, stride, padding, pool) -> bool:
+    """Whether teacher_conv2d(..., pool=pool) fuses the max pool into the conv
+    (fedagg_conv_pool_fusable: the LDS-resident kernel for 1 or 3 input
+    channels; SimpleCNN's conv1 -> relu -> max_pool2d(2, 2, padding=1))."""
+    f = _pool_flags(pool)
+    if f <= 0:
+        return False
+    s = conv_shape(x_shape, out_channels, kernel_size, stride, padding)
+    return bool(_native.load().fedagg_conv_pool_fusable(ctypes.byref(s), f))
+
+
 def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
                    out_channels: int, kernel_size, stride, padding, shared: bool,
-                   relu: bool = False, gather: bool = False) -> torch.Tensor:
+                   relu: bool = False, gather: bool = False, pool=None) -> torch.Tensor:
     """One nn.Conv2d (groups 1, dilation 1, zero padding) of the K teachers
     whose flat parameter vectors are the rows of ``slab`` ([K, P]), as an
     implicit GEMM on the matrix cores (fedagg_teacher_conv2d_f32).  ``x``:
     [M, C, H, W] shared by every teacher (``shared``) or [K, M, C, H, W].
     ``padding`` = (top, bottom, left, right) zeros.  Returns
     y [K, M, OC, OH, OW] (ReLU applied when ``relu``).  b_off = -1: no bias.
-    ``gather``: the im2col-gather kernel even where the LDS one applies."""
+    ``gather``: the im2col-gather kernel even where the LDS one applies.
+    ``pool`` = (2, 2, 2, 2, p, p), p in {0, 1}: the max pool after the layer
+    fused into its store (conv_pool_fusable must hold); y is then the pooled
+    [K, M, OC, PH, PW], the same bits as pad_lrn_maxpool(y, pool=pool)."""
     _require_hip_f32(x, "x")
     _require_hip_f32(slab, "slab")
     if slab.dim() != 2 or not _rows_contiguous(slab) or x.device != slab.device:
@@ -466,13 +491,21 @@ def teacher_conv2d(x: torch.Tensor, slab: torch.Tensor, w_off: int, b_off: int,
     R = C * KH * KW
     if w_off < 0 or w_off + out_channels * R > P or (b_off >= 0 and b_off + out_channels > P):
         raise ValueError("layer offsets outside the parameter vector")
+    pflags = _pool_flags(pool)
+    if pflags < 0:
+        raise ValueError(f"pool {pool} is not a 2 x 2 / stride 2 max pool with padding 0 or 1")
     shape = _native.Conv2dShape(M, C, H, W, out_channels, KH, KW, sh, sw, pt, pl, OH, OW)
+    flags = ((_native.FEDAGG_RELU if relu else 0) | (_native.FEDAGG_CONV_GATHER if gather else 0)
+             | pflags)
+    if pflags:
+        if not _native.load().fedagg_conv_pool_fusable(ctypes.byref(shape), flags):
+            raise ValueError("the conv kernel does not fuse this pool for this shape")
+        ph = pool[4]
+        OH, OW = (OH + 2 * ph - 2) // 2 + 1, (OW + 2 * ph - 2) // 2 + 1
     y = torch.empty((K, M, out_channels, OH, OW), dtype=torch.float32, device=x.device)
     rc = _native.load().fedagg_teacher_conv2d_f32(
         x.data_ptr(), 0 if shared else M * C * H * W, slab.data_ptr(), _row_pitch(slab), w_off,
-        b_off, K, ctypes.byref(shape), y.data_ptr(),
-        (_native.FEDAGG_RELU if relu else 0) | (_native.FEDAGG_CONV_GATHER if gather else 0),
-        _stream_ptr(x.device))
+        b_off, K, ctypes.byref(shape), y.data_ptr(), flags, _stream_ptr(x.device))
     check(rc, "fedagg_teacher_conv2d_f32")
     return y
 

@@ -110,6 +110,16 @@ extern "C" {
  * LDS-resident one applies (A/B and its own tests; same results up to the
  * chain order fedagg_conv_order reports) */
 #define FEDAGG_CONV_GATHER 0x800000
+/* fedagg_teacher_conv2d_f32: the 2 x 2 / stride 2 max pool that follows the
+ * layer (after its ReLU) fused into the store, padding 0, or 1 with
+ * FEDAGG_CONV_POOL_PAD1 (SimpleCNN's F.max_pool2d(x, 2, 2, padding=1),
+ * simple_models.py:156-159): y is then [K, M, OC, PH, PW], PH = (OH + 2p -
+ * 2) / 2 + 1 (PW alike), max over each window's members inside the conv
+ * output (-inf padding), NaN propagating, in window order -- the same bits as
+ * the conv followed by fedagg_pad_lrn_maxpool_f32 with that pool.  Only for
+ * the shapes fedagg_conv_pool_fusable accepts (else FEDAGG_EINVAL). */
+#define FEDAGG_CONV_MAXPOOL2  0x2000000
+#define FEDAGG_CONV_POOL_PAD1 0x4000000
 
 /* negative error codes */
 #define FEDAGG_EINVAL   (-22) /* bad size / null pointer / bad flag combination */
@@ -208,7 +218,8 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
  * input shared by all teachers); W_k = params + k*params_kstride + w_off
  * ([OC, C, KH, KW] row-major, the teacher's flat vector); b_off = -1: no
  * bias.  y is [K, M, OC, OH, OW] contiguous.  flags: FEDAGG_RELU,
- * FEDAGG_CONV_GATHER.  Each output is an exact f32 fmaf chain from +0.0f,
+ * FEDAGG_CONV_GATHER, FEDAGG_CONV_MAXPOOL2 (| FEDAGG_CONV_POOL_PAD1).
+ * Each output is an exact f32 fmaf chain from +0.0f,
  * then one bias add: normwise, not bitwise, equal to a CPU conv.  The chain's
  * order is what fedagg_conv_order reports for the shape:
  *   0  (the im2col-gather kernel, and the LDS-resident kernel for C = 1 or 3
@@ -234,6 +245,11 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
 /* Reductions per LDS stage the conv kernel takes for R = C*KH*KW (16 or 32;
  * the exact chain is the same either way). Host-side, no device access. */
 int fedagg_conv_stage(int64_t R);
+
+/* 1 if fedagg_teacher_conv2d_f32 fuses the max pool FEDAGG_CONV_MAXPOOL2 (|
+ * FEDAGG_CONV_POOL_PAD1) asks for on this shape (the LDS-resident kernel for
+ * C = 1 or 3, stride 1, 3 x 3 / 5 x 5), else 0. Host-side, no device access. */
+int fedagg_conv_pool_fusable(const fedagg_conv2d_shape* shape, int flags);
 
 /* Chain order of fedagg_teacher_conv2d_f32 for this shape and flags: 0 for
  * the (c, kh, kw) order, else the channel chunk cc (see above). Host-side. */

@@ -23,7 +23,7 @@ def header_functions():
 
 def header_defines():
     out = {}
-    for m in re.finditer(r"#define\s+(FEDAGG_[A-Z_]+)\s+\(?(-?0x[0-9A-Fa-f]+|-?\d+)\)?",
+    for m in re.finditer(r"#define\s+(FEDAGG_[A-Z0-9_]+)\s+\(?(-?0x[0-9A-Fa-f]+|-?\d+)\)?",
                          open(HEADER).read()):
         out[m.group(1)] = int(m.group(2), 0)
     return out
@@ -44,7 +44,7 @@ def test_header_declares_the_abi():
         "fedagg_reduce_rows_f32",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_pack_segments_f32",
         "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_teacher_conv2d_f32",
-        "fedagg_conv_stage", "fedagg_conv_order", "fedagg_pool_output",
+        "fedagg_conv_stage", "fedagg_conv_order", "fedagg_conv_pool_fusable", "fedagg_pool_output",
         "fedagg_pad_lrn_maxpool_f32",
         "fedagg_finalize_f32",
         "fedagg_fedavg_sgd_f32",
@@ -67,7 +67,9 @@ def test_python_mirror_matches_header(lib):
     d = header_defines()
     assert _native.ABI_VERSION == d["FEDAGG_ABI_VERSION"] == lib.fedagg_abi_version()
     for name in ("FEDAGG_INIT", "FEDAGG_FINALIZE", "FEDAGG_NT", "FEDAGG_SCALAR",
-                 "FEDAGG_UNROLL_SHIFT", "FEDAGG_VPT_SHIFT", "FEDAGG_MAP_SHIFT", "FEDAGG_EINVAL"):
+                 "FEDAGG_UNROLL_SHIFT", "FEDAGG_VPT_SHIFT", "FEDAGG_MAP_SHIFT", "FEDAGG_EINVAL",
+                 "FEDAGG_RELU", "FEDAGG_CONV_GATHER", "FEDAGG_POOL_PLANES", "FEDAGG_CONV_MAXPOOL2",
+                 "FEDAGG_CONV_POOL_PAD1"):
         assert getattr(_native, name) == d[name], name
     assert set(_native.exported_symbols()) == set(header_functions())
 

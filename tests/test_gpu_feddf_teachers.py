@@ -501,3 +501,109 @@ def test_simplecnn2_replay_at_reference_size():
                 torch.linalg.vector_norm(want.double()))
     assert rel <= 1e-5, rel
     assert (prog.conv_launches, prog.pool_launches, prog.linear_launches) == (2, 2, 3)
+
+
+@pytest.mark.parametrize("M,C,H,W,OC,pads,K,pp,relu,shared", [
+    (64, 1, 28, 28, 32, (1, 1, 1, 1), 40, 1, True, True),    # SimpleCNN conv1 -> pool(2, 2, pad 1)
+    (64, 1, 28, 28, 32, (1, 1, 1, 1), 3, 1, True, False),    # per-teacher inputs
+    (64, 3, 24, 24, 64, (2, 2, 2, 2), 20, 0, True, True),    # RGB, both channel halves, pad 0
+    (7, 3, 17, 13, 70, (2, 2, 2, 2), 30, 1, False, True),    # odd planes, no ReLU, 2 oc tiles
+    (5, 1, 9, 12, 20, (1, 1, 1, 1), 9, 0, False, False),     # OH = 7 odd: pool drops a row
+    (1, 1, 6, 6, 3, (1, 1, 1, 1), 2, 1, True, True),         # one image, a few windows
+])
+def test_conv_with_fused_maxpool_is_conv_then_pool_bitwise(M, C, H, W, OC, pads, K, pp, relu,
+                                                           shared):
+    """FEDAGG_CONV_MAXPOOL2: the 2 x 2 / stride 2 max pool in the flat conv's
+    store gives the same bits as the conv kernel followed by the pool pass
+    (and torch's max_pool2d on that output), for both pool paddings, with
+    and without the fused ReLU, and the pooled shape torch gives."""
+    from fedsim_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(M + C + OC + K + pp)
+    kern = (5, 5)
+    R = C * 25
+    P = 3 + OC * R + OC
+    slab = torch.randn(K, P, device=DEV, generator=g)
+    x = torch.randn(M, C, H, W, device=DEV, generator=g)
+    if not shared:
+        x = x.expand(K, *x.shape).contiguous() + 0.1 * torch.randn(K, *x.shape, device=DEV,
+                                                                    generator=g)
+    pool = (2, 2, 2, 2, pp, pp)
+    assert ops.conv_pool_fusable(x.shape, OC, kern, (1, 1), pads, pool)
+    y = ops.teacher_conv2d(x, slab, 3, 3 + OC * R, OC, kern, (1, 1), pads, shared=shared,
+                           relu=relu)
+    want = ops.pad_lrn_maxpool(y, (0, 0, 0, 0), None, pool)
+    got = ops.teacher_conv2d(x, slab, 3, 3 + OC * R, OC, kern, (1, 1), pads, shared=shared,
+                             relu=relu, pool=pool)
+    assert got.shape == want.shape
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+    tw = torch.nn.functional.max_pool2d(y.reshape(-1, *y.shape[-2:]), 2, 2, pp)
+    assert torch.equal(got.reshape(tw.shape).view(torch.int32), tw.view(torch.int32))
+
+
+def test_conv_with_fused_maxpool_special_values():
+    """NaN / inf in a teacher's weights reach the pooled output as the
+    two-pass result has them (max_pool2d's NaN rule, in window order)."""
+    from fedsim_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(99)
+    M, C, H, W, OC, K = 4, 1, 10, 10, 8, 3
+    R = C * 25
+    P = OC * R + OC
+    slab = torch.randn(K, P, device=DEV, generator=g)
+    slab[0, 0] = float("nan")                # channel 0 of teacher 0: NaN everywhere
+    slab[1, R * 3 + 7] = float("inf")        # channel 3 of teacher 1: +-inf / NaN mixes
+    slab[2, OC * R + 5] = float("-inf")      # bias of channel 5, teacher 2: -inf plane
+    x = torch.randn(M, C, H, W, device=DEV, generator=g)
+    x[1, 0, 4, 4] = 0.0
+    for relu in (False, True):
+        for pp in (0, 1):
+            pool = (2, 2, 2, 2, pp, pp)
+            y = ops.teacher_conv2d(x, slab, 0, OC * R, OC, (5, 5), (1, 1), (1, 1, 1, 1),
+                                   shared=True, relu=relu)
+            want = ops.pad_lrn_maxpool(y, (0, 0, 0, 0), None, pool)
+            got = ops.teacher_conv2d(x, slab, 0, OC * R, OC, (5, 5), (1, 1), (1, 1, 1, 1),
+                                     shared=True, relu=relu, pool=pool)
+            assert torch.equal(got.view(torch.int32), want.view(torch.int32)), (relu, pp)
+
+
+def test_fused_maxpool_rejected_where_not_taken():
+    """Only the flat (1- / 3-channel) kernel fuses the pool; anything else is
+    refused before a launch (the replay keeps the pool pass)."""
+    from fedsim_amd import ops
+
+    assert not ops.conv_pool_fusable((2, 32, 14, 14), 64, (5, 5), (1, 1), (1, 1, 1, 1),
+                                     (2, 2, 2, 2, 1, 1))  # SimpleCNN conv2: chunked kernel
+    assert not ops.conv_pool_fusable((2, 1, 28, 28), 32, (5, 5), (1, 1), (1, 1, 1, 1),
+                                     (3, 3, 2, 2, 0, 0))  # not a 2 x 2 pool
+    slab = torch.zeros(2, 64 * 32 * 25 + 64, device=DEV)
+    with pytest.raises(ValueError):
+        ops.teacher_conv2d(torch.zeros(2, 32, 14, 14, device=DEV), slab, 0, -1, 64, (5, 5),
+                           (1, 1), (1, 1, 1, 1), shared=True, pool=(2, 2, 2, 2, 1, 1))
+
+
+def test_simplecnn_replay_fuses_conv1_pool():
+    """The reference's SimpleCNN (fedsim_amd.models restatement, Resize leaf
+    included) replays with conv1's ReLU + max_pool2d(2, 2, padding=1) in the
+    conv's store: one pool pass left (conv2's), outputs within fp32 rounding
+    of each teacher's own forward."""
+    from fedsim_amd import models
+    from fedsim_amd.distributed.centralized.training import teacher_program as TP
+    from fedsim_amd.utils import vector_to_named_parameters_like
+
+    torch.manual_seed(21)
+    model = models.SimpleCNN().to(DEV)
+    named = list(model.named_parameters())
+    base = torch.cat([p.detach().reshape(-1) for _, p in named])
+    K = 12
+    slab = torch.stack([base + 0.01 * torch.randn_like(base) for _ in range(K)])
+    prog = TP.build(model, named, slab)
+    assert prog is not None
+    x = torch.randn(64, 1, 28, 28, device=DEV)
+    got = prog(x)
+    assert prog.fused_pools == 1 and prog.pool_launches == 1 and prog.conv_launches == 2
+    want = torch.stack([functional_call(model, vector_to_named_parameters_like(slab[k], named),
+                                        (x,)) for k in range(K)])
+    err = float(torch.linalg.vector_norm((got - want).double()) /
+                torch.linalg.vector_norm(want.double()))
+    assert err <= 1e-5, err

@@ -26,7 +26,7 @@ def linear_stub(x, slab, w_off, b_off, in_f, out_f, shared, relu=False):
     return torch.relu(y) if relu else y
 
 
-def conv_stub(x, slab, w_off, b_off, oc, kernel, stride, pads, shared, relu=False):
+def conv_stub(x, slab, w_off, b_off, oc, kernel, stride, pads, shared, relu=False, pool=None):
     K = slab.shape[0]
     C = x.shape[-3]
     W = slab[:, w_off:w_off + oc * C * kernel[0] * kernel[1]].view(K, oc, C, *kernel)
@@ -38,7 +38,10 @@ def conv_stub(x, slab, w_off, b_off, oc, kernel, stride, pads, shared, relu=Fals
         ys.append(torch.nn.functional.conv2d(torch.nn.functional.pad(xs[k], (l, r, t, b)), W[k],
                                              bias, stride))
     y = torch.stack(ys)
-    return torch.relu(y) if relu else y
+    y = torch.relu(y) if relu else y
+    if pool is not None:
+        y = pool_stub(y, (0, 0, 0, 0), None, pool)
+    return y
 
 
 def pool_stub(x, pads, lrn, pool):
@@ -317,3 +320,29 @@ def test_random_ops_in_the_graph_are_detected():
         slab = torch.zeros(2, sum(p.numel() for p in m.parameters()))
         prog = TP.build(m, list(m.named_parameters()), slab, impl=STUBS)
         assert prog is not None and prog.has_random_ops is random, cls
+
+
+def test_conv_fuses_the_following_2x2_max_pool():
+    """SimpleCNN's conv -> relu -> max_pool2d(2, 2, padding=1) runs as one
+    conv launch with the pooled store when the kernel takes the shape
+    (fedagg_conv_pool_fusable); SimpleCNN2's pad / LRN / 3x3 pool chains do
+    not fuse.  Same outputs either way."""
+    from fedsim_amd import models
+
+    fusing = types.SimpleNamespace(teacher_linear=linear_stub, teacher_conv2d=conv_stub,
+                                   pad_lrn_maxpool=pool_stub,
+                                   conv_pool_fusable=lambda *a: a[1] <= 32)  # conv1 only
+    for name, kw, shape, fused in (("SimpleCNN", {}, (2, 1, 28, 28), 1),
+                                   ("SimpleCNN2", dict(num_classes=100), (2, 3, 24, 24), 0)):
+        torch.manual_seed(2)
+        model = getattr(models, name)(**kw)
+        named = list(model.named_parameters())
+        base = torch.cat([p.detach().reshape(-1) for _, p in named])
+        slab = torch.stack([base + 0.01 * torch.randn_like(base) for _ in range(3)])
+        x = torch.randn(*shape)
+        plain = TP.build(model, named, slab, impl=STUBS)(x)
+        prog = TP.build(model, named, slab, impl=fusing)
+        got = prog(x)
+        torch.testing.assert_close(got, plain, rtol=0, atol=0)
+        assert prog.fused_pools == fused
+        assert prog.conv_launches == 2 and prog.pool_launches == 2 - fused

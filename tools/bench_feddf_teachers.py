@@ -2,7 +2,7 @@
 the Linear layers on the matrix cores (teacher_program.py) against the
 whole-model torch.vmap over the teacher slab, for the reference's model
 shapes (SimpleMLP 784-200-200-10 and SimpleCNN on MNIST, SimpleCNN2 on
-CIFAR-100), B = 64
+CIFAR-100; fedsim_amd.models, each with the reference's Resize leaf), B = 64
 (the server's test_batch_size), K teachers.  Kernel time from HIP events,
 median of repeated calls.
 
@@ -15,71 +15,13 @@ import sys
 
 import numpy as np
 import torch
-from torch import nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedsim_amd.distributed.centralized.training.feddf import TeacherEnsemble  # noqa: E402
 
 
-class SimpleMLP(nn.Module):  # fedsim/models/simple_models.py:23 (Resize is the identity at 28x28)
-    def __init__(self):
-        super().__init__()
-        self.fc1 = nn.Linear(784, 200)
-        self.fc2 = nn.Linear(200, 200)
-        self.classifier = nn.Linear(200, 10)
-
-    def forward(self, x):
-        x = torch.flatten(x, 1)
-        x = torch.relu(self.fc1(x))
-        x = torch.relu(self.fc2(x))
-        return self.classifier(x)
-
-
-class SimpleCNN(nn.Module):  # fedsim/models/simple_models.py:80-162, MNIST (1 x 28 x 28)
-    def __init__(self):
-        super().__init__()
-        self.conv1 = nn.Conv2d(1, 32, 5, padding=1)
-        self.conv2 = nn.Conv2d(32, 64, 5, padding=1)
-        self.fc = nn.Linear(64 * 7 * 7, 512)
-        self.classifier = nn.Linear(512, 10)
-
-    def forward(self, x):
-        F = torch.nn.functional
-        x = F.relu(self.conv1(x))
-        x = F.max_pool2d(x, kernel_size=2, stride=2, padding=1)
-        x = F.relu(self.conv2(x))
-        x = F.max_pool2d(x, kernel_size=2, stride=2, padding=1)
-        x = x.view(x.shape[0], -1)
-        x = F.relu(self.fc(x))
-        return self.classifier(x)
-
-
-class SimpleCNN2(nn.Module):  # fedsim/models/simple_models.py:165-255, num_classes=100
-    """The reference's forward after its Resize to 24 x 24 (inputs are fed at
-    24 x 24 here; torchvision is not installed)."""
-
-    def __init__(self):
-        super().__init__()
-        self.conv1 = nn.Conv2d(3, 64, 5, padding="same")
-        self.conv2 = nn.Conv2d(64, 64, 5, padding="same")
-        self.fc1 = nn.Linear(64 * 6 * 6, 384)
-        self.fc2 = nn.Linear(384, 192)
-        self.classifier = nn.Linear(192, 100)
-
-    def forward(self, x):
-        F = torch.nn.functional
-        x = F.relu(self.conv1(x))
-        x = F.pad(x, (0, 1, 0, 1), value=0)
-        x = F.local_response_norm(x, size=4, alpha=0.001 / 9)
-        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=0)
-        x = F.relu(self.conv2(x))
-        x = F.local_response_norm(x, size=4, alpha=0.001 / 9)
-        x = F.pad(x, (0, 1, 0, 1), value=0)
-        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=0)
-        x = x.view(x.shape[0], -1)
-        x = F.relu(self.fc1(x))
-        x = F.relu(self.fc2(x))
-        return self.classifier(x)
+from fedsim_amd.models import SimpleCNN, SimpleCNN2, SimpleMLP  # noqa: E402  (the reference's
+# classes restated, Resize leaf included: fedsim/models/simple_models.py:23-256)
 
 
 def timed(fn, reps=10):
@@ -106,7 +48,7 @@ def main():
     dev = torch.device("cuda:0")
     for name, cls, shape in (("SimpleMLP", SimpleMLP, (64, 1, 28, 28)),
                              ("SimpleCNN", SimpleCNN, (64, 1, 28, 28)),
-                             ("SimpleCNN2", SimpleCNN2, (64, 3, 24, 24))):
+                             ("SimpleCNN2", lambda: SimpleCNN2(num_classes=100), (64, 3, 24, 24))):
         if name not in a.models.split(","):
             continue
         torch.manual_seed(0)
@@ -125,7 +67,9 @@ def main():
                 vm = TeacherEnsemble(model, teachers, dev, program=False)
                 t_vmap = timed(lambda: vm.mean_logits(x), a.reps)
                 del vm
+            st = ens.stats()
             print(json.dumps(dict(model=name, P=P, K=K, B=shape[0], program_kept=kept,
+                                  fallback=st["reason"], fused_pools=st["fused_pools"],
                                   matrix_core_ms=t_prog, vmap_ms=t_vmap,
                                   speedup=(t_vmap / t_prog) if t_prog and t_vmap else None)),
                   flush=True)
