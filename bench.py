@@ -668,6 +668,8 @@ def _main(a, quiet):
                  "cyclically; FedAvg int weights U{50..600})"),
         "config": dict(info, mode_flag=a.mode),
     }
+    result["world_size_seen"] = rk.dist.get_world_size() if rk.dist is not None else 1
+    result["backend"] = rk.dist.get_backend() if rk.dist is not None else None
     if rk.rehearsal:
         result["rehearsal"] = "cpu/gloo launcher rehearsal, per-rank reduce = " + a.rehearsal_stub
         result["roofline"] = None
@@ -675,8 +677,6 @@ def _main(a, quiet):
         if a.one_gpu_rehearsal:
             result["rehearsal"] = ("one-GPU launcher rehearsal: %d ranks share cuda:0 over "
                                    "gloo (not a scaling number)" % rk.world)
-        result["world_size_seen"] = rk.dist.get_world_size() if rk.dist is not None else 1
-        result["backend"] = rk.dist.get_backend() if rk.dist is not None else None
         achieved = nbytes / (kern_ms_max * 1e-3) / 1e9
         result["roofline"] = {
             "bound": "hbm",

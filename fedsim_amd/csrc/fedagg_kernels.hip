@@ -2039,10 +2039,13 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   extern __shared__ float lds[];
   float* sW = lds;
   float* sX = lds + kTC_OC * RW;
-  const ConvTile tile = conv_tile_order();
-  const int64_t k = tile.z;
-  const int oc0 = tile.y * kTC_OC;
-  const int pxt = tile.x;
+  // plain dispatch order here: this kernel's input is shared by every
+  // teacher and its weights are a few KB, so the XCD order (conv_tile_order)
+  // has nothing to save, and it measured 2 % slower on SimpleCNN2's conv1
+  // (2.249 vs 2.198 ms at K=500, the two builds interleaved, profiles/r03pmc/)
+  const int64_t k = blockIdx.z;
+  const int oc0 = blockIdx.y * kTC_OC;
+  const int pxt = blockIdx.x;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;

@@ -56,3 +56,44 @@ def test_world_mismatch_rejected():
                         "--rehearsal-stub", "tests.bench_stub:reduce", "--K", "2", "--P", "64"],
                        cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("mode", ["param", "strong", "allreduce"])
+def test_driver_command_at_8_ranks(mode):
+    """The driver's own 8-GPU form, rehearsed on CPU/gloo: torch.distributed.run
+    --nproc-per-node 8 --master-addr 127.0.0.1 --master-port P bench.py --gpus 8.
+    Exactly one JSON line (rank 0's), world_size_seen 8, n_gpus 8, the
+    mode's scaling and decomposition (readiness)."""
+    port = _free_port()
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), os.path.join(REPO, "bench.py"), "--gpus", "8", "--mode", mode,
+                        "--rehearsal-stub", "tests.bench_stub:reduce", "--K", "9", "--P", "1000",
+                        "--steps", "2", "--warmup", "1", "--pool-rows", "4"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["world_size_seen"] == 8
+    assert d["scaling"] == ("strong" if mode == "strong" else "weak")
+    assert d["backend"] == "gloo"
+    if mode == "allreduce":  # (the all-reduce's HIP-event share: tests/test_gpu_bench.py)
+        assert d["config"]["clients_K"] == 9 * 8
+        assert d["config"]["parallelism"] == "client-shard8+allreduce"
+    if mode == "strong":
+        assert d["config"]["params_total"] == 1000
+    assert "cpu_baseline" not in d or d["cpu_baseline"] is None  # rank 0 at N=1 only

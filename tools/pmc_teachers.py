@@ -6,7 +6,8 @@ over tools/pmc_calib (8 GiB read / written once per kernel, so factor =
 half of a streaming read on gfx950).  Algorithmic bytes per launch: the
 layer's input read once and its output written once.
 
-python tools/pmc_teachers.py gpurun_out/r02pmc > profiles/r02pmc/teacher_traffic.json
+python tools/pmc_teachers.py gpurun_out/r02pmc [run prefix, default "teach"] \
+    > profiles/r02pmc/teacher_traffic.json
 """
 import collections
 import csv
@@ -21,7 +22,7 @@ ALG = {  # kernel name prefix -> (label, algorithmic read bytes, write bytes)
     "k_pad_lrn_maxpool_q<4, 3>": ("pool1 (per-block planes)", 4.0 * K * M * 64 * 576, 4.0 * K * M * 64 * 144),
     "k_pad_lrn_maxpool_slide<4, 1, 16>": ("pool2 (sliding window)", 4.0 * K * M * 64 * 144, 4.0 * K * M * 64 * 36),
     "k_pad_lrn_maxpool_q<4, 1>": ("pool2 (per-block planes)", 4.0 * K * M * 64 * 144, 4.0 * K * M * 64 * 36),
-    "k_teacher_conv2d_flat<5, 3, 16>": ("conv1 (flat, LDS)", 4.0 * (M * 3 * 576 + K * 64 * 76), 4.0 * K * M * 64 * 576),
+    "k_teacher_conv2d_flat<5, 3, 16,": ("conv1 (flat, LDS)", 4.0 * (M * 3 * 576 + K * 64 * 76), 4.0 * K * M * 64 * 576),
     "k_teacher_conv2d_lds<5, 4, 8>": ("conv2 (chunked, LDS)", 4.0 * (K * M * 64 * 144 + K * 64 * 1601), 4.0 * K * M * 64 * 144),
 }
 
@@ -46,10 +47,11 @@ def factor(d, counter, kernel):
 
 def main():
     root = sys.argv[1]
+    run = sys.argv[2] if len(sys.argv) > 2 else "teach"
     ff = factor(os.path.join(root, "calib_fetch"), "FETCH_SIZE", "calib_read<1>")
     fw = factor(os.path.join(root, "calib_write"), "WRITE_SIZE", "calib_write<1>")
-    fetch = per_dispatch(os.path.join(root, "teach_fetch"), "FETCH_SIZE")
-    write = per_dispatch(os.path.join(root, "teach_write"), "WRITE_SIZE")
+    fetch = per_dispatch(os.path.join(root, run + "_fetch"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(root, run + "_write"), "WRITE_SIZE")
     rows = []
     for prefix, (label, ar, aw) in ALG.items():
         fv = [v for n, vs in fetch.items() if prefix in n for v in vs]
@@ -61,7 +63,7 @@ def main():
         rows.append(dict(kernel=prefix, layer=label, hbm_read_bytes=r, hbm_write_bytes=w,
                          alg_read_bytes=ar, alg_write_bytes=aw, read_over_alg=r / ar,
                          write_over_alg=w / aw, launches=len(fv)))
-    print(json.dumps(dict(K=K, M=M, fetch_factor_4B=ff, write_factor_4B=fw, kernels=rows),
+    print(json.dumps(dict(K=K, M=M, run=run, fetch_factor_4B=ff, write_factor_4B=fw, kernels=rows),
                      indent=1))
 
 
