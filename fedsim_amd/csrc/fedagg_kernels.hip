@@ -1574,7 +1574,7 @@ __global__ __launch_bounds__(256) void k_teacher_linear(
       const int64_t m = m0 + wave * 16 + (lane >> 4) * 4 + r;
       if (m >= M) continue;
       float v = acc[j][r] + bias;
-      if (relu) v = v > 0.f ? v : 0.f;
+      if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
       yk[m * out + n] = v;
     }
   }
@@ -1764,7 +1764,7 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
         const int64_t oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
         if (oc >= s.OC) continue;
         float v = acc[a][b][e] + (bk ? bk[oc] : 0.f);
-        if (relu) v = v > 0.f ? v : 0.f;
+        if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
         yp[oc * OHW] = v;
       }
     }
@@ -1974,7 +1974,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_LDS_
         const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
         if (oc >= OC) continue;
         float v = acc[a][b][e] + (bk ? bk[oc] : 0.f);
-        if (relu) v = v > 0.f ? v : 0.f;
+        if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
         yp[int64_t(oc) * OHW] = v;
       }
     }
@@ -2159,7 +2159,6 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-  [[maybe_unused]] const bool hi = oc0 + 32 < OC;  // wave-uniform
 #pragma unroll
   for (int st = 0; st < RP; ++st) {
     const int r0 = 2 * st, r1 = 2 * st + 1;
@@ -2182,10 +2181,12 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
       const float a1 = pa[32 * RW + 2 * st];
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[0], acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv[1], acc[0][1], 0, 0, 0);
-      if (hi) {  // the upper 32 output channels exist
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[0], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[1], acc[1][1], 0, 0, 0);
-      }
+      // the upper 32 output channels unconditionally: a tile with fewer
+      // than 33 channels reads zero weights there and never stores them, and
+      // a branch per k step kept the compiler from issuing the next step's
+      // LDS reads under this step's MFMAs
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[0], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[1], acc[1][1], 0, 0, 0);
     }
   }
   // epilogue: each bias value loaded once for both pixel groups
@@ -2220,7 +2221,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
         for (int b = 0; b < NPG; ++b) {
           if (!pin[b]) continue;
           float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias;
-          if (relu) v = v > 0.f ? v : 0.f;
+          if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
           if (!inside[b]) v = -__builtin_huge_valf();
           v = pool_dpp_max<0xB1>(v);  // members (0, 1) and (2, 3): quad_perm [1, 0, 3, 2]
           v = pool_dpp_max<0x4E>(v);  // then (01, 23): quad_perm [2, 3, 0, 1]
@@ -2251,7 +2252,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
       for (int b = 0; b < NPG; ++b) {
         if (!pin[b]) continue;
         float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias;
-        if (relu) v = v > 0.f ? v : 0.f;
+        if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
         yp[b][int64_t(oc) * OHW] = v;
       }
     }

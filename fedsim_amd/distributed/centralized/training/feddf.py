@@ -168,25 +168,32 @@ class TeacherEnsemble(object):
         if self.program is None:
             return self._vmap_logits(x)
         if self._checked:
-            return self.program(x)
+            try:
+                return self.program(x)
+            except Exception as e:  # noqa: BLE001 - e.g. a later batch's shape
+                self.program = None
+                self._fall_back(f"the replay raised {type(e).__name__} on a later batch: {e}")
+                return self._vmap_logits(x)
         # first use: the program must reproduce the vmap'd forward (same
         # graph, f32 matrix-core arithmetic: normwise), else it is dropped
         ref = self._vmap_logits(x)
         try:
             got = self.program(x)
-            err = float(torch.linalg.vector_norm((got - ref).double().nan_to_num())) \
-                if got.shape == ref.shape else float("inf")
-            bound = 1e-4 * float(torch.linalg.vector_norm(ref.double().nan_to_num())) + 1e-30
-            ok = (err <= bound
-                  and bool(torch.isfinite(got).all() == torch.isfinite(ref).all()))
-            why = None if ok else (
-                f"its first batch differs from the vmap'd forward (normwise {err / bound * 1e-4:.3g}"
-                f" > 1e-4)" if got.shape == ref.shape else
-                f"its output shape {tuple(got.shape)} is not {tuple(ref.shape)}")
+            why = None
+            if got.shape != ref.shape:
+                why = f"its output shape {tuple(got.shape)} is not {tuple(ref.shape)}"
+            elif not bool((torch.isfinite(got) == torch.isfinite(ref)).all()):
+                why = "its first batch has non-finite values where the vmap'd forward has not"
+            else:
+                err = float(torch.linalg.vector_norm((got - ref).double().nan_to_num()))
+                ref_n = float(torch.linalg.vector_norm(ref.double().nan_to_num()))
+                if err > 1e-4 * ref_n + 1e-30:
+                    why = (f"its first batch differs from the vmap'd forward (normwise "
+                           f"{err / max(ref_n, 1e-30):.3g} > 1e-4)")
         except Exception as e:  # noqa: BLE001 - a graph the replay cannot run: keep vmap
-            got, ok, why = None, False, f"the replay raised {type(e).__name__}: {e}"
+            got, why = None, f"the replay raised {type(e).__name__}: {e}"
         self._checked = True
-        if not ok:
+        if why is not None:
             self.program = None
             self._fall_back(why)
             return ref

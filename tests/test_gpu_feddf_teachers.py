@@ -607,3 +607,32 @@ def test_simplecnn_replay_fuses_conv1_pool():
     err = float(torch.linalg.vector_norm((got - want).double()) /
                 torch.linalg.vector_norm(want.double()))
     assert err <= 1e-5, err
+
+
+def test_fused_relu_is_torch_relu_bitwise():
+    """The ReLU fused into the Linear / Conv2d kernels is torch.relu's
+    (x < 0 ? 0 : x): NaN stays NaN, so a teacher with non-finite outputs
+    gives the reference's values (the kernels' fmaf chains start from +0, so
+    their pre-activations are never -0)."""
+    from fedsim_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(77)
+    K, M, in_f, out_f = 3, 8, 5, 7
+    slab = torch.randn(K, in_f * out_f + out_f, device=DEV, generator=g)
+    slab[0, 0] = float("nan")                      # a NaN output column for teacher 0
+    x = torch.randn(M, in_f, device=DEV, generator=g)
+    plain = ops.teacher_linear(x, slab, 0, in_f * out_f, in_f, out_f, shared=True)
+    fused = ops.teacher_linear(x, slab, 0, in_f * out_f, in_f, out_f, shared=True, relu=True)
+    want = torch.relu(plain)
+    assert torch.isnan(want).any()
+    assert torch.equal(fused.view(torch.int32), want.view(torch.int32))
+    C, OC = 1, 4
+    cs = torch.randn(K, OC * C * 9 + OC, device=DEV, generator=g)
+    cs[2, 0] = float("nan")
+    xi = torch.randn(2, C, 6, 6, device=DEV, generator=g)
+    plain = ops.teacher_conv2d(xi, cs, 0, OC * 9, OC, (3, 3), (1, 1), (1, 1, 1, 1), shared=True)
+    fused = ops.teacher_conv2d(xi, cs, 0, OC * 9, OC, (3, 3), (1, 1), (1, 1, 1, 1), shared=True,
+                               relu=True)
+    want = torch.relu(plain)
+    assert torch.isnan(want).any()
+    assert torch.equal(fused.view(torch.int32), want.view(torch.int32))
