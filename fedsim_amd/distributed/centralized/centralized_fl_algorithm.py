@@ -34,6 +34,22 @@ def _distributed_world() -> int:
     return d.get_world_size() if d.is_available() and d.is_initialized() else 1
 
 
+def _to_host(obj):
+    """A client-storage value made picklable across ranks: tensors to host
+    memory, tagged with where they lived."""
+    if isinstance(obj, torch.Tensor):
+        return ("__fedsim_tensor__", obj.detach().cpu(), obj.device.type, obj.requires_grad)
+    return obj
+
+
+def _from_host(obj, device):
+    if isinstance(obj, tuple) and len(obj) == 4 and obj[0] == "__fedsim_tensor__":
+        _, t, kind, rg = obj
+        t = t.to(device) if kind == "cuda" and device.type == "cuda" else t
+        return t.requires_grad_(rg) if rg else t
+    return obj
+
+
 def _distributed_rank() -> int:
     d = torch.distributed
     return d.get_rank() if d.is_available() and d.is_initialized() else 0
@@ -61,6 +77,8 @@ class CentralFLAlgorithm(object):
         *args,
         aggregator_factory=None,
         shard_over=None,
+        shard_clients=None,
+        client_reduction="chain",
         progress=False,
         **kwargs,
     ):
@@ -108,6 +126,27 @@ class CentralFLAlgorithm(object):
         # loop, one process per GPU), a ProcessGroup, or a list of local
         # devices (one process driving several GPUs).  Opt-in: ranks of a
         # group that run different simulations must not be sharded together.
+        # shard_clients (not in the reference): split each round's CLIENTS
+        # over the ranks of a process group ("group" = the default group, or a
+        # ProcessGroup): rank r trains one contiguous block of the sampled
+        # clients, every rank receives every message (other ranks' vectors as
+        # stand-ins) and the blocks are combined by ``client_reduction``:
+        # "chain" (bit-exact) or "allreduce" (RCCL, normwise).  See
+        # fedsim_amd.sharding.ClientShardedSerialAggregator.
+        if shard_clients is not None:
+            if aggregator_factory is not None or shard_over is not None:
+                raise ValueError("shard_clients excludes aggregator_factory and shard_over")
+            from ...sharding import ClientShardedSerialAggregator
+
+            world = (torch.distributed.get_world_size(
+                None if shard_clients == "group" else shard_clients)
+                if torch.distributed.is_available() and torch.distributed.is_initialized()
+                else 1)
+            kw = dict(expected_rows=-(-sample_count // world), borrow=True,
+                      mode=client_reduction)
+            if shard_clients != "group":
+                kw["group"] = shard_clients
+            aggregator_factory = partial(ClientShardedSerialAggregator, **kw)
         if aggregator_factory is None:
             kw = dict(expected_rows=sample_count, borrow=True)
             if shard_over is None:
@@ -243,14 +282,18 @@ class CentralFLAlgorithm(object):
             # clients that train on the GPU vectorize straight into this
             # round's HBM slab (utils/slab_rows.py)
             with round_aggregator(round_serial_aggregator):
-                for client_id in self._sample_clients():
-                    client_msg = self._send_to_server(client_id)
-                    success = self._receive_from_client(client_msg, round_serial_aggregator,
-                                                        round_appendix_aggregator)
-                    del client_msg  # the aggregator may hold the message's tensor
-                    if not success:
-                        diverged = True
-                        break
+                if hasattr(round_serial_aggregator, "client_block"):
+                    diverged = self._client_sharded_round(round_serial_aggregator,
+                                                          round_appendix_aggregator)
+                else:
+                    for client_id in self._sample_clients():
+                        client_msg = self._send_to_server(client_id)
+                        success = self._receive_from_client(client_msg, round_serial_aggregator,
+                                                            round_appendix_aggregator)
+                        del client_msg  # the aggregator may hold the message's tensor
+                        if not success:
+                            diverged = True
+                            break
             if diverged:
                 # drop the round's slab without launching
                 del round_serial_aggregator
@@ -262,6 +305,61 @@ class CentralFLAlgorithm(object):
             self._at_round_end(score_aggregator)
             self._server_memory.write("rounds", cur_round + round_num + 1, silent=True)
         return score_aggregator.pop_all()
+
+    def _client_sharded_round(self, agg, appendix_aggregator) -> bool:
+        """One round's clients under a ClientShardedSerialAggregator: this rank
+        trains its block of the sampled clients, then every rank receives all
+        the round's messages in the reference's order (other ranks' vectors as
+        RemoteRow stand-ins), so the server state evolves identically on every
+        rank.  Clients' own storages (AdaBest / FedDyn drift state) are
+        shared with every rank after the round.  Returns ``diverged``."""
+        from ...sharding import RemoteRow
+
+        clients = self._sample_clients()  # same seed, same list on every rank
+        lo, hi = agg.client_block(len(clients))
+        local = {p: self._send_to_server(clients[p]) for p in range(lo, hi)}
+        remote = agg.exchange(local, len(clients))
+        diverged = False
+        for p in range(len(clients)):
+            client_msg = local.pop(p) if p in local else remote[p]
+            remote[p] = None
+            success = self._receive_from_client(client_msg, agg, appendix_aggregator)
+            del client_msg
+            if not success:
+                diverged = True
+                break
+        local.clear()
+        self._share_client_memory(agg, clients[lo:hi])
+        for key in appendix_aggregator.keys():
+            if any(isinstance(v, RemoteRow) for v in appendix_aggregator.get_values(key)):
+                raise NotImplementedError(
+                    "client-sharded rounds keep each client vector on the rank that trained it; "
+                    f"{key!r} keeps every client's vector (FedDF): use shard_over instead")
+        return diverged
+
+    def _share_client_memory(self, agg, trained) -> None:
+        """Every rank gets the client storages this round's other ranks wrote
+        (tensors travel through host memory and land on this rank's device)."""
+        import torch.distributed as dist
+
+        def portable(st):
+            return [(k, _to_host(obj), rp, wp) for k, (obj, rp, wp) in st._storage.items()]
+
+        if agg._solo:
+            return
+        mine = {cid: portable(self._client_memory[cid]) for cid in trained
+                if len(self._client_memory[cid].get_all_keys())}
+        every = [None] * agg.world_size
+        dist.all_gather_object(every, mine, group=agg._group)
+        dev = agg._reduce_device()
+        for r, mem in enumerate(every):
+            if r == agg.rank:
+                continue
+            for cid, items in mem.items():
+                st = Storage()
+                for k, obj, rp, wp in items:
+                    st._storage[k] = (_from_host(obj, dev), rp, wp)
+                self._client_memory[cid] = st
 
     def _at_round_start(self) -> None:
         self.user_methods["at_round_start"](self._server_memory)

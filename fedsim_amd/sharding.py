@@ -453,3 +453,350 @@ class ShardedSerialAggregator(SerialAggregator):
         """[lo, hi) columns this rank reduces for a tensor key."""
         e = self._entry(key)
         return (e.lo, e.hi) if isinstance(e, _ShardEntry) else None
+
+
+# ---------------------------------------------------------------------------
+# client-sharded rounds on the plugin surface
+# ---------------------------------------------------------------------------
+class RemoteRow(torch.Tensor):
+    """Stand-in for a client vector that lives on another rank of a
+    client-sharded round: shape and dtype only, no storage (a wrapper over
+    the meta device).  Copies and detaches keep the stand-in (the reference's
+    ``clone().detach().data``, training/utils.py:34, feddf.py:87); any
+    arithmetic on it raises, naming the rank that holds the vector."""
+
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    @staticmethod
+    def __new__(cls, shape, dtype, src_type: str, owner: int):
+        t = torch.Tensor._make_wrapper_subclass(cls, tuple(shape), dtype=dtype, device="meta")
+        t.src_type = src_type  # "cuda" / "cpu": where the client produced it
+        t.owner = owner
+        return t
+
+    def __repr__(self):
+        return "RemoteRow(shape=%s, owner=rank %d)" % (tuple(self.shape), self.owner)
+
+    @classmethod
+    def __torch_dispatch__(cls, func, types, args=(), kwargs=None):
+        src = args[0]
+        if func in _REMOTE_KEEP:
+            return RemoteRow(src.shape, src.dtype, src.src_type, src.owner)
+        raise RuntimeError(
+            f"{func} on a client vector held by rank {src.owner} of a client-sharded round: "
+            "only its SerialAggregator can use it")
+
+
+_aten = torch.ops.aten
+_REMOTE_KEEP = (_aten.clone.default, _aten.detach.default, _aten.alias.default)
+
+
+class _RowStub(object):
+    """Picklable description of a message tensor (RemoteRow on arrival)."""
+
+    __slots__ = ("shape", "dtype", "src_type", "owner")
+
+    def __init__(self, t: torch.Tensor, owner: int):
+        self.shape, self.dtype, self.src_type, self.owner = (
+            tuple(t.shape), t.dtype, t.device.type, owner)
+
+
+class _ScalarTensor(object):
+    """A 0-dim message tensor (a metric) sent by value."""
+
+    __slots__ = ("value", "src_type")
+
+    def __init__(self, t: torch.Tensor):
+        self.value, self.src_type = t.detach().cpu(), t.device.type
+
+
+def _skeleton(obj, owner: int):
+    if isinstance(obj, torch.Tensor):
+        return _ScalarTensor(obj) if obj.dim() == 0 else _RowStub(obj, owner)
+    if isinstance(obj, dict):
+        return {k: _skeleton(v, owner) for k, v in obj.items()}
+    if type(obj) in (list, tuple):
+        return type(obj)(_skeleton(v, owner) for v in obj)
+    return obj
+
+
+def _flesh(obj, device):
+    if isinstance(obj, _RowStub):
+        return RemoteRow(obj.shape, obj.dtype, obj.src_type, obj.owner)
+    if isinstance(obj, _ScalarTensor):
+        return obj.value.to(device) if obj.src_type == "cuda" and device.type == "cuda" \
+            else obj.value
+    if isinstance(obj, dict):
+        return {k: _flesh(v, device) for k, v in obj.items()}
+    if type(obj) in (list, tuple):
+        return type(obj)(_flesh(v, device) for v in obj)
+    return obj
+
+
+def _global_rank(group, r: int) -> int:
+    return r if group is None else dist.get_global_rank(group, r)
+
+
+def _via_host(group, t: torch.Tensor) -> bool:
+    """gloo moves host tensors only: HIP tensors of a gloo group go through
+    host memory (RCCL groups move them in HBM over xGMI)."""
+    return t.device.type == "cuda" and dist.get_backend(group) == dist.Backend.GLOO
+
+
+def _send(t, dst, group):
+    dist.send(t.cpu() if _via_host(group, t) else t, dst=dst, group=group)
+
+
+def _recv(t, src, group):
+    if _via_host(group, t):
+        h = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.recv(t, src=src, group=group)
+
+
+def _broadcast(t, src, group):
+    if _via_host(group, t):
+        h = t.cpu()
+        dist.broadcast(h, src=src, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src, group=group)
+
+
+def _all_reduce_sum(t, group):
+    if _via_host(group, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+
+
+class _ClientShardEntry(_TensorEntry):
+    """A tensor key of a client-sharded round: the Python weight sum over
+    every client of the round in arrival order (the reference's ``cur_w``),
+    which ranks hold rows in that order, and this rank's own rows as a
+    one-GPU entry (exact, arrival order)."""
+
+    def __init__(self, agg: "ClientShardedSerialAggregator", shape, src_type: str):
+        self.agg = agg
+        self.shape = tuple(shape)
+        self.P = 1
+        for d in self.shape:
+            self.P *= d
+        self.src_type = src_type
+        self.dev = agg._reduce_device()
+        self.out_device = self.dev if src_type == "cuda" else torch.device("cpu")
+        self.cur_w = 0
+        self.local = None
+        self.owners = []  # ranks holding rows, in arrival order (one run each)
+        self.sum = None
+
+    def _owner(self, r: int) -> None:
+        if not self.owners or self.owners[-1] != r:
+            self.owners.append(r)
+
+    def add(self, value: torch.Tensor, weight) -> None:
+        new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
+        if tuple(value.shape) != self.shape:
+            raise ValueError(
+                f"tensor of shape {tuple(value.shape)} added to a key aggregating {self.shape}")
+        if isinstance(value, RemoteRow):
+            self._owner(value.owner)
+        else:
+            if self.local is None:
+                self.local = self.agg._local_entry(self._key, value)
+            self.local.add(value, weight)
+            self._owner(self.agg.rank)
+        self.cur_w = new_w
+
+    def _weighted(self) -> bool:
+        return not (self.cur_w is None or self.cur_w == 0)
+
+    def _global_sum(self) -> torch.Tensor:
+        """The raw sum over every rank's rows (collective: every rank calls
+        it for the same key, as SPMD ``optimize`` does)."""
+        if self.sum is not None:
+            return self.sum
+        agg = self.agg
+        me = agg.rank
+        if agg._solo:
+            buf = self.local.partial(None)
+        elif agg.mode == "allreduce":
+            buf = (self.local.partial(None) if self.local is not None
+                   else torch.zeros(self.P, dtype=torch.float32, device=self.dev))
+            _all_reduce_sum(buf, agg._group)
+        else:
+            if len(set(self.owners)) != len(self.owners):
+                raise RuntimeError("client_reduction='chain' needs each rank's clients to be one "
+                                   "contiguous run of the round's arrival order")
+            if me in self.owners:
+                i = self.owners.index(me)
+                acc_in = None
+                if i > 0:
+                    acc_in = torch.empty(self.P, dtype=torch.float32, device=self.dev)
+                    _recv(acc_in, _global_rank(agg._group, self.owners[i - 1]), agg._group)
+                buf = self.local.partial(acc_in)
+                if i + 1 < len(self.owners):
+                    _send(buf, _global_rank(agg._group, self.owners[i + 1]), agg._group)
+            else:
+                buf = torch.empty(self.P, dtype=torch.float32, device=self.dev)
+            _broadcast(buf, _global_rank(agg._group, self.owners[-1]), agg._group)
+        self.local = None
+        self.sum = buf
+        return buf
+
+    def _average(self) -> torch.Tensor:
+        s = self._global_sum()
+        if not self._weighted():
+            return s.clone()
+        if s.device.type == "cuda":
+            return ops.finalize(s, self.cur_w)
+        return s / ops.fl32(self.cur_w)  # CPU gloo rehearsal: ATen's true divide
+
+    def _deliver(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.view(self.shape)
+        return t if t.device == self.out_device else t.to(self.out_device)
+
+    def get(self) -> torch.Tensor:
+        return self._deliver(self._average())
+
+    def get_sum(self) -> torch.Tensor:
+        return self._deliver(self._global_sum().clone())
+
+    def pop(self, on_device: bool = False) -> torch.Tensor:
+        avg = self._average()
+        self.sum = None
+        return avg.view(self.shape) if on_device else self._deliver(avg)
+
+    def pop_step(self, step: ops.ServerStep) -> None:
+        avg = self._average().reshape(-1)
+        self.sum = None
+        self.agg._apply_step(step, avg)
+
+
+class ClientShardedSerialAggregator(SerialAggregator):
+    """Client-sharded drop-in for the reference SerialAggregator
+    (fedsim/utils/aggregators.py:11-144) for a round loop whose clients are
+    split over the ranks of a process group, one process per GPU: each rank
+    trains one contiguous block of the round's sampled clients (the
+    expensive part of a FedSim round runs N-way parallel) and reduces their
+    vectors in HBM; the blocks are then combined with a collective (SURVEY
+    §8e, config 5's decomposition on the plugin surface).
+
+    The round driver (CentralFLAlgorithm(..., shard_clients=...)) hands every
+    rank every client's message in the reference's arrival order, the
+    vectors of other ranks' clients as ``RemoteRow`` stand-ins, so every
+    rank runs ``receive_from_client`` for the whole round and keeps the same
+    server state (scalar metrics, AdaBest's running statistics, weight sums)
+    with the reference's arithmetic.  ``add`` of a stand-in records its
+    weight and owner; ``add`` of a local vector goes to this rank's one-GPU
+    entry (ring slab / slab rows / borrowed rows, exact order).
+
+    ``get`` / ``get_sum`` / ``pop`` / ``pop_step`` of a tensor key are
+    collective (every rank calls them, as the SPMD ``optimize`` does):
+      * ``mode="chain"`` (default): the running sum passes from rank to rank
+        in arrival order (rank r adds its rows onto rank r-1's sum; N-1
+        point-to-point hops of 4P bytes), then the last rank's sum is
+        broadcast: every column sums k = 0..K-1 in order, BIT-EXACT;
+      * ``mode="allreduce"``: each rank's partial sum from +0, one RCCL
+        all-reduce(sum), the divide by fl32(W): reordered, parity normwise
+        (<= 1e-6 relative).
+    Every rank then applies the server step to its own copy of the cloud
+    (same operands, same kernel: same bits), so all ranks hold the new model.
+
+    Args:
+        group: the torch.distributed group (default: the default group).
+        mode: "chain" or "allreduce".
+        entry_factory / step_impl: TEST HOOKS (the per-rank rows and the
+            server step on CPU, so the protocol runs over gloo).
+        **kwargs: SerialAggregator's options for this rank's rows.
+    """
+
+    def __init__(self, group=None, mode: str = "chain", entry_factory: Optional[Callable] = None,
+                 step_impl: Optional[Callable] = None, **kwargs) -> None:
+        if mode not in ("chain", "allreduce"):
+            raise ValueError("mode must be 'chain' or 'allreduce'")
+        super().__init__(**kwargs)
+        self._group = group
+        self._rank, self._world = _group_rank_world(group)
+        # one process and no process group: the same round, no collectives
+        self._solo = not (dist.is_available() and dist.is_initialized())
+        self.mode = mode
+        self._entry_factory = entry_factory
+        self._step_impl = step_impl
+
+    @property
+    def rank(self) -> int:
+        return self._rank
+
+    @property
+    def world_size(self) -> int:
+        return self._world
+
+    def client_block(self, n: int):
+        """[lo, hi): the positions of the round's n sampled clients this rank
+        trains (one contiguous block each, in rank order)."""
+        return shard_range(n, self._rank, self._world)
+
+    def _reduce_device(self) -> torch.device:
+        if self._entry_factory is not None:
+            return torch.device("cpu")
+        if self._opts.device is not None:
+            return torch.device(self._opts.device)
+        return torch.device("cuda", torch.cuda.current_device())
+
+    def _local_entry(self, key, value: torch.Tensor):
+        if self._entry_factory is not None:
+            return self._entry_factory(value, self)
+        dev = self._reduce_device()
+        return _DeviceEntry(value, dev, self._opts, self, out_device=dev)
+
+    def _apply_step(self, step: ops.ServerStep, avg: torch.Tensor) -> None:
+        if self._step_impl is not None:
+            self._step_impl(step, avg)
+        else:
+            step.apply(avg if avg.device == step.cloud.device else avg.to(step.cloud.device))
+
+    def add(self, key, value, weight=None):
+        if isinstance(value, torch.Tensor) and value.dim() > 0:
+            e = self._members.get(key)
+            if e is None:
+                src = value.src_type if isinstance(value, RemoteRow) else value.device.type
+                e = _ClientShardEntry(self, value.shape, src)
+                e._key = key
+                e.add(value, weight)  # may raise (weight None): the key is not created
+                self._members[key] = e
+                return
+            if not isinstance(e, _ClientShardEntry):
+                raise TypeError(f"key {key!r} aggregates scalars; got an N-d tensor")
+            e.add(value, weight)
+            return
+        super().add(key, value, weight)
+
+    def exchange(self, local_msgs: dict, n: int) -> list:
+        """Every rank's client messages of this round, position by position:
+        this rank's own as given, the others' rebuilt from what their ranks
+        sent (tensors as RemoteRow stand-ins, 0-dim tensors and everything
+        else by value).  Collective."""
+        if self._solo:
+            return [None] * n
+        mine = {p: _skeleton(m, self._rank) for p, m in local_msgs.items()}
+        every = [None] * self._world
+        dist.all_gather_object(every, mine, group=self._group)
+        dev = self._reduce_device()
+        out = [None] * n
+        for r, msgs in enumerate(every):
+            if r == self._rank:
+                continue
+            for p, m in msgs.items():
+                out[p] = _flesh(m, dev)
+        return out
+
+    def reserve(self, key, P, device):
+        """No reserved rows: a rank trains all its clients before any of them
+        is received, and a ring hands out one row at a time; the clients'
+        fresh vectors are borrowed at ``add`` instead (no copy)."""
+        return None

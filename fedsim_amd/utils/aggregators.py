@@ -438,6 +438,24 @@ class _DeviceEntry(_TensorEntry):
         self.acc = None
         return out
 
+    def partial(self, acc_in: Optional[torch.Tensor], W=None) -> torch.Tensor:
+        """This key's rows reduced in arrival order ONTO ``acc_in`` (None:
+        from +0), divided by fl32(W) when W is given; releases the rows.  The
+        per-rank step of a client-sharded chain (fedsim_amd.sharding): rank r
+        continues rank r-1's running sum, so no row may have been drained
+        into the accumulator before (it would have started from +0)."""
+        if acc_in is not None:
+            if self.acc is not None:
+                raise RuntimeError(
+                    "rows were already drained from +0 (ring full): a chained partial sum "
+                    "needs every row pending; raise slab_bytes / max_rows")
+            self.acc = acc_in.reshape(-1)
+        self._flush(final_W=W)
+        out = self.acc
+        self.release()
+        self.acc = None
+        return out
+
     def pop_step(self, step: ops.ServerStep) -> None:
         """pop(on_device=True) followed by step.apply(avg), fused into the last
         drain when rows are pending, the step's operands allow it and the

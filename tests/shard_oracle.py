@@ -58,3 +58,30 @@ class OracleEntry(_TensorEntry):
         avg_out = step.operands.get("avg_out")
         if avg_out is not None:
             avg_out.copy_(avg)
+
+
+class ChainOracleEntry(OracleEntry):
+    """This rank's rows of a ClientShardedSerialAggregator key, reduced by the
+    oracle onto the running sum of the ranks before it (the chain step)."""
+
+    def partial(self, acc_in, W=None):
+        ai = None if acc_in is None else np.ascontiguousarray(acc_in.numpy()).copy()
+        return torch.from_numpy(ref.reduce(np.stack(self.rows), self.ws, acc_in=ai, W=W))
+
+    def release(self):
+        self.rows, self.ws = [], []
+
+
+def oracle_step(step, avg):
+    """The server step of a client-sharded round on CPU operands: the ABI's
+    own step description handed to the oracle (as OracleEntry.pop_step)."""
+    CALLS["pop_step"] += 1
+    avg = avg.contiguous()
+    a, s = step.args, step.sgd
+    ref.lib().ref_server_step_f32(a.algo, avg.data_ptr(), a.coef, a.cloud, a.aux, a.avg_prev,
+                                  a.momentum_buf, a.momentum_init, a.grad_out, s.neg_lr,
+                                  s.momentum, s.one_minus_dampening, s.weight_decay,
+                                  s.nesterov, s.maximize, step.P)
+    avg_out = step.operands.get("avg_out")
+    if avg_out is not None:
+        avg_out.copy_(avg)
