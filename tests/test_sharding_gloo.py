@@ -510,6 +510,19 @@ def _client_extras_worker(rank, world, port, outdir):
         res["diverged_cloud"] = alg.get_server_storage().read("cloud_params").detach().tolist()
         res["diverged_scores"] = {k: float(v) for k, v in scores.items()}
 
+        # (4) real local SGD (the clients' own send_to_server): every rank
+        # trains only its block and ends the round with the same model
+        random.seed(S.RANDOM_SEED)
+        torch.manual_seed(S.TORCH_SEED)  # the same initial model on every rank
+        alg = training.FedAvg(data_manager=S.TensorDataManager(), metric_logger=None,
+                              num_clients=S.NUM_CLIENTS, sample_scheme="uniform",
+                              sample_rate=S.SAMPLE_RATE, model_def=S.TinyModel, epochs=1,
+                              criterion_def="CrossEntropyScore", device="cpu",
+                              aggregator_factory=factory)
+        torch.manual_seed(S.TORCH_SEED + 100 + rank)  # each rank's own training RNG
+        alg.train(rounds=1)
+        res["local_sgd_cloud"] = alg.get_server_storage().read("cloud_params").detach().tolist()
+
         # (3) FedDF keeps every client vector: refused on every rank
         feddf = S.make_algorithm(training.FedDF)
         alg = make(feddf)
@@ -529,7 +542,9 @@ def test_client_sharded_state_divergence_and_refusal():
     may train that client elsewhere); a diverged client stops the whole
     training on every rank at the same round with the same state; FedDF,
     which keeps every client's vector, is refused with NotImplementedError
-    rather than run on stand-ins."""
+    rather than run on stand-ins; with real local SGD (each rank drawing
+    its own random numbers) every rank still ends each round with the same
+    model."""
     import json
 
     world = 2
