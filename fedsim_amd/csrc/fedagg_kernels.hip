@@ -1464,7 +1464,23 @@ constexpr int kTL_N = 64;  // output columns (features) per workgroup
 constexpr int kTL_K = 32;  // inputs per LDS stage
 constexpr int kTL_PAD = 1;
 
-__global__ __launch_bounds__(256) void k_teacher_linear(
+#ifndef FEDAGG_TL_WPE  // waves per SIMD the Linear kernel is compiled for (A/B builds; 0: the
+#define FEDAGG_TL_WPE 0  // compiler's choice)
+#endif
+#ifndef FEDAGG_TL_BUF  // the buffer-descriptor Linear kernel where it applies (A/B builds: 0 = off)
+#define FEDAGG_TL_BUF 1
+#endif
+#ifndef FEDAGG_TL_WIDE_IN  // inputs above which a Linear layer counts as wide (see the launch)
+#define FEDAGG_TL_WIDE_IN 1024
+#endif
+#ifndef FEDAGG_TL_PAD_KB  // LDS reserved per workgroup of a wide layer: 4 per CU (A/B: 0 = none)
+#define FEDAGG_TL_PAD_KB 20
+#endif
+__global__ __launch_bounds__(256)
+#if FEDAGG_TL_WPE
+__attribute__((amdgpu_waves_per_eu(FEDAGG_TL_WPE, FEDAGG_TL_WPE)))
+#endif
+void k_teacher_linear(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t M, int64_t in, int64_t out,
     float* __restrict__ y, int64_t n_tiles, int64_t m_tiles, int relu) {
@@ -1576,6 +1592,105 @@ __global__ __launch_bounds__(256) void k_teacher_linear(
       float v = acc[j][r] + bias;
       if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
       yk[m * out + n] = v;
+    }
+  }
+}
+
+// The same Linear tile with every staging load through a buffer descriptor
+// (32-bit lane offsets fixed for the whole K loop, the stage advanced by the
+// scalar offset, rows past M / out and the tail past ``in`` reading 0 from
+// outside the descriptor's range).  The generic kernel above computes 64-bit
+// addresses per load (101 VGPRs, 4 waves per SIMD): its 32-input stages then
+// wait on memory with only one stage in flight (SimpleMLP's fc1: 212 us per
+// 1000 teachers, 47 TFLOP/s).  Here the tile needs about half the registers,
+// so twice the workgroups are resident to hide the same latency.  Same LDS
+// layout and MFMA sequence: the same bits.  Taken when every teacher's x and
+// W rows are 16-B aligned and the per-teacher extents fit 32-bit offsets.
+__global__ __launch_bounds__(256) void k_teacher_linear_buf(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, int M, int in, int out,
+    float* __restrict__ y, int n_tiles, int m_tiles, int relu) {
+  __shared__ float sx[kTL_M][kTL_K + kTL_PAD];
+  __shared__ float sw[kTL_N][kTL_K + kTL_PAD];
+  const int tiles = n_tiles * m_tiles;
+  const int tile = blockIdx.x;
+  const int k = tile / tiles;
+  const int rem = tile - k * tiles;
+  const int m0 = (rem / n_tiles) * kTL_M;
+  const int n0 = (rem % n_tiles) * kTL_N;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  constexpr uint32_t kOut = 0x80000000u;  // > num_records: reads 0
+  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + int64_t(k) * x_kstride), static_cast<short>(0), M * in * 4,
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(params + int64_t(k) * params_kstride + w_off), static_cast<short>(0),
+      out * in * 4, 0x00020000);
+  // thread t stages inputs 4 (t % 8) .. + 3 of rows t / 8 and t / 8 + 32
+  const int c4 = 4 * (t & 7);
+  uint32_t xo[2], wo[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = (t >> 3) + 32 * j;
+    xo[j] = (m0 + r < M) ? static_cast<uint32_t>(((m0 + r) * in + c4) * 4) : kOut;
+    wo[j] = (n0 + r < out) ? static_cast<uint32_t>(((n0 + r) * in + c4) * 4) : kOut;
+  }
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rx[2], rw[2];
+  auto fetch = [&](int i0) {
+    const bool in_row = i0 + c4 < in;  // in % 4 == 0: the whole quad is in or out
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      rx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            xres, static_cast<int>(in_row ? xo[j] : kOut),
+                                            i0 * 4, 0));
+      rw[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            wres, static_cast<int>(in_row ? wo[j] : kOut),
+                                            i0 * 4, 0));
+    }
+  };
+  fetch(0);
+  const int row = lane & 15;
+  const int kk = lane >> 4;
+  for (int i0 = 0; i0 < in; i0 += kTL_K) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sx[(t >> 3) + 32 * j][c4 + q] = rx[j][q];
+        sw[(t >> 3) + 32 * j][c4 + q] = rw[j][q];
+      }
+    __syncthreads();
+    if (i0 + kTL_K < in) fetch(i0 + kTL_K);
+#pragma unroll
+    for (int s4 = 0; s4 < kTL_K / 4; ++s4) {
+      const float a = sx[wave * 16 + row][4 * s4 + kk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float b = sw[j * 16 + row][4 * s4 + kk];
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  const float* bk = b_off >= 0 ? params + int64_t(k) * params_kstride + b_off : nullptr;
+  float* yk = y + int64_t(k) * M * out;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + j * 16 + (lane & 15);
+    if (n >= out) continue;
+    const float bias = bk ? bk[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wave * 16 + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+      float v = acc[j][r] + bias;
+      if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
+      yk[int64_t(m) * out + n] = v;
     }
   }
 }
@@ -2927,8 +3042,31 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
   const int64_t kMaxGridX = (int64_t(1) << 32) / 256 - 1;
   if (per > kMaxGridX) return FEDAGG_EINVAL;
   const int64_t kchunk = kMaxGridX / per;
+  // the buffer-descriptor kernel: every teacher's rows 16-B aligned, the
+  // per-teacher extents within 32-bit byte offsets
+  const bool buf = FEDAGG_TL_BUF && (in % 4) == 0 && (x_kstride % 4) == 0 &&
+                   (params_kstride % 4) == 0 && (w_off % 4) == 0 &&
+                   (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(params) % 16) == 0 && M * in < (int64_t(1) << 29) &&
+                   out * in < (int64_t(1) << 29) && per < (int64_t(1) << 30);
   for (int64_t k0 = 0; k0 < K; k0 += kchunk) {
     const int64_t kn = K - k0 < kchunk ? K - k0 : kchunk;
+    if (buf) {
+      // wide layers stream each teacher's W once (weight-bound): at eight
+      // workgroups per CU their 2048 concurrent row streams lose DRAM locality
+      // (SimpleCNN's fc, in = 3136: 1049 vs 960 us for the generic kernel at
+      // four per CU), so they reserve LDS for four per CU
+      const size_t pad = (in > FEDAGG_TL_WIDE_IN) ? size_t(FEDAGG_TL_PAD_KB) * 1024 : 0;
+      hipLaunchKernelGGL(k_teacher_linear_buf, dim3(static_cast<unsigned>(kn * per)), dim3(256), pad,
+                         static_cast<hipStream_t>(stream), x + k0 * x_kstride, x_kstride,
+                         params + k0 * params_kstride, params_kstride, w_off, b_off,
+                         static_cast<int>(M), static_cast<int>(in), static_cast<int>(out),
+                         y + k0 * M * out, static_cast<int>(n_tiles), static_cast<int>(m_tiles),
+                         (flags & FEDAGG_RELU) ? 1 : 0);
+      const int rc = static_cast<int>(hipGetLastError());
+      if (rc) return rc;
+      continue;
+    }
     hipLaunchKernelGGL(k_teacher_linear, dim3(static_cast<unsigned>(kn * per)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), x + k0 * x_kstride, x_kstride,
                        params + k0 * params_kstride, params_kstride, w_off, b_off, M, in, out,
