@@ -2113,9 +2113,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_LDS_
 #define FEDAGG_FLAT_WAVES 4   // builds: 8 stages each image once per 512 pixels but runs two
 #endif                        // workgroups per CU; conv1 2.33 vs 2.13 ms, profiles/r02xf)
 constexpr int kFlatThreads = 64 * FEDAGG_FLAT_WAVES;
-#ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds;
-#define FEDAGG_FLAT_WPE 4  // 4: SimpleCNN2 conv1 2.26 ms vs 2.52 ms with 3, profiles/r02x3)
-#endif
+#ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds): 4 -> 3 lost
+#define FEDAGG_FLAT_WPE 5  // 10 % (r02x3); with the compact row staging 5 fit without spills
+#endif                     // (<= 96 VGPRs): SimpleCNN2 conv1 2.058 vs 2.217 ms (profiles/r03l); 6 spills
 // POOL: the 2 x 2 / stride 2 max pool (padding ppad = 0 or 1) that follows
 // the layer is fused into the store (FEDAGG_CONV_MAXPOOL2; SimpleCNN's
 // relu -> max_pool2d(2, 2, padding=1), simple_models.py:156-159).  The
@@ -2140,7 +2140,7 @@ template <int KS, int CI, int XM, bool HALF, bool POOL>
 __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
-    float* __restrict__ y, int relu, int ppad) {
+    int nrows, float* __restrict__ y, int relu, int ppad) {
   constexpr int TAPS = KS * KS;
   constexpr int R = CI * TAPS;
   constexpr int RP = (R + 1) / 2;    // k steps
@@ -2167,7 +2167,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int H = static_cast<int>(s.H), W = static_cast<int>(s.W);
   const int OW = static_cast<int>(s.OW);
   const int OHW = static_cast<int>(s.OH * s.OW);
-  const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = OW + KS - 1, HpWp = Hp * Wp;
+  const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = OW + KS - 1;
   const int HW = H * W;
   const int OH = static_cast<int>(s.OH);
   // pooled planes (POOL): PH x PW windows of 2 x 2, four pixel slots each
@@ -2192,6 +2192,11 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   // Only the padded rows the tile's output rows read are staged (and
   // zeroed): from row_lo of the first image to row_hi of the last one
   // (a 256-pixel tile needs ~1/3 of the two 24 x 24 images it touches).
+  // In LDS they are packed per channel as stacked padded rows g = slot * Hp
+  // + row, from g = row_lo on: sX[c][g - row_lo][col], ``nrows`` rows per
+  // channel (the host's bound for any tile), so the workgroup's LDS holds
+  // only those rows and more workgroups fit on a CU.
+  const int CP = nrows * Wp;  // channel pitch in sX
   const int xtot = nslot * CI * HW;
   const int pend = (px0 + TPX < NPX ? px0 + TPX : NPX) - 1;
   // slot of the tile's last image; the padded rows its pixels read (POOL:
@@ -2199,12 +2204,9 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int last = (POOL ? (pend >> 2) / PHW : pend / OHW) - m_lo;
   const int row_lo = POOL ? 0 : (px0 - m_lo * OHW) / OW;
   const int row_hi = POOL ? Hp - 1 : (pend - (m_lo + last) * OHW) / OW + KS - 1;
-  for (int pc = 0; pc < (last + 1) * CI; ++pc) {
-    const int slot = pc / CI;
-    const int lo = slot == 0 ? row_lo : 0;
-    const int hi = slot == last ? row_hi : Hp - 1;
-    for (int q = lo * Wp + t; q < (hi + 1) * Wp; q += kFlatThreads) sX[pc * HpWp + q] = 0.f;
-  }
+  const int nrow = last * Hp + row_hi - row_lo + 1;  // rows this tile stages (<= nrows)
+  for (int c = 0; c < CI; ++c)
+    for (int q = t; q < nrow * Wp; q += kFlatThreads) sX[c * CP + q] = 0.f;
   float rx[XM];
   int lidx[XM];
 #pragma unroll
@@ -2217,7 +2219,8 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
     const int prow = h + pt;
     const bool need = e < xtot && slot <= last && (slot > 0 || prow >= row_lo) &&
                       (slot < last || prow <= row_hi);
-    lidx[i] = need ? (sc * Hp + prow) * Wp + (hw - h * W) + pl : -1;
+    lidx[i] = need ? ((sc - slot * CI) * nrows + slot * Hp + prow - row_lo) * Wp + (hw - h * W) + pl
+                   : -1;
     rx[i] = need ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                           xres, static_cast<int>(e * 4u + x_tile4), 0, 0))
                  : 0.f;
@@ -2265,7 +2268,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
       oh = ohw / OW;
       ow = ohw - oh * OW;
     }
-    xb[b] = (m - m_lo) * CI * HpWp + oh * Wp + ow;
+    xb[b] = ((m - m_lo) * Hp + oh - row_lo) * Wp + ow;
   }
   f32x16 acc[2][2];
 #pragma unroll
@@ -2277,8 +2280,8 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
 #pragma unroll
   for (int st = 0; st < RP; ++st) {
     const int r0 = 2 * st, r1 = 2 * st + 1;
-    const int o0 = (r0 / TAPS) * HpWp + ((r0 % TAPS) / KS) * Wp + r0 % KS;
-    const int o1 = r1 < R ? (r1 / TAPS) * HpWp + ((r1 % TAPS) / KS) * Wp + r1 % KS : 0;
+    const int o0 = (r0 / TAPS) * CP + ((r0 % TAPS) / KS) * Wp + r0 % KS;
+    const int o1 = r1 < R ? (r1 / TAPS) * CP + ((r1 % TAPS) / KS) * Wp + r1 % KS : 0;
     const int ob = kk ? o1 : o0;
     const float a0 = pa[2 * st];
     float bv[NPG];
@@ -2379,6 +2382,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
 // thread, nslot: images a 256-pixel tile can touch, lds: bytes.
 struct ConvLdsPlan {
   int ks, cc, xm, nslot;
+  int nrows;  // flat kernel: stacked padded rows staged per channel
   size_t lds;
 };
 
@@ -2403,11 +2407,20 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
     const int64_t xall = s.C * fslot * HW;
     if (xall <= 16 * kFlatThreads) {
       const int64_t rw = (s.C * ks * ks + 1) / 2 * 2 + 1;
+      // rows a tile reads: its output rows (a run of tpx pixels meets at most
+      // ceil((tpx - 1) / OW) + 1 of them; image boundaries are row
+      // boundaries) plus KS - 1 halo rows per image; POOL stages whole images
+      int64_t nrows = fslot * Hp;
+      if (pool_pad < 0) {
+        const int64_t rows_out = (tpx - 1 + s.OW - 1) / s.OW + 1;
+        if (rows_out + fslot * (ks - 1) < nrows) nrows = rows_out + fslot * (ks - 1);
+      }
       p->ks = static_cast<int>(ks);
       p->cc = 0;
       p->xm = xall <= 8 * kFlatThreads ? 8 : 16;
       p->nslot = static_cast<int>(fslot);
-      p->lds = static_cast<size_t>(kTC_OC * rw + fslot * s.C * Hp * Wp) * sizeof(float);
+      p->nrows = static_cast<int>(nrows);
+      p->lds = static_cast<size_t>(kTC_OC * rw + s.C * nrows * Wp) * sizeof(float);
       if (p->lds <= 64 * 1024) return true;
     }
   }
@@ -2426,6 +2439,7 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
   p->cc = cc;
   p->xm = xm;
   p->nslot = static_cast<int>(nslot);
+  p->nrows = 0;
   p->lds = static_cast<size_t>(kTC_OC * (cc * ks * ks + 1) + nslot * cc * Hp * Wp) * sizeof(float);
   return p->lds <= 64 * 1024;
 }
@@ -3170,7 +3184,8 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
   } while (0)
 #define FEDAGG_CONV_FLAT_H(KS, CI, XM, HF, PL)                                                \
   hipLaunchKernelGGL((k_teacher_conv2d_flat<KS, CI, XM, HF, PL>), gflat, dim3(kFlatThreads), plan.lds, st, xk, \
-                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu, ppad)
+                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, plan.nrows, yk, \
+                     relu, ppad)
       if (plan.cc == 0) {
         const bool half = s.OC <= 32;
         const int64_t tpx = (half ? 2 : 1) * kFlatThreads;
