@@ -317,8 +317,19 @@ class CentralFLAlgorithm(object):
 
         clients = self._sample_clients()  # same seed, same list on every rank
         lo, hi = agg.client_block(len(clients))
-        local = {p: self._send_to_server(clients[p]) for p in range(lo, hi)}
-        remote = agg.exchange(local, len(clients))
+        local, failure = {}, None
+        try:
+            for p in range(lo, hi):
+                local[p] = self._send_to_server(clients[p])
+        except Exception as e:  # noqa: BLE001 - re-raised below, after the exchange
+            failure, local = e, {}
+        # every rank reaches the exchange, so a failing client cannot leave
+        # the others blocked in it; then every rank raises
+        remote = agg.exchange(local, len(clients), failed=failure is not None)
+        if failure is not None:
+            raise failure
+        if remote is None:
+            raise RuntimeError("a client of another rank of this client-sharded round failed")
         diverged = False
         for p in range(len(clients)):
             client_msg = local.pop(p) if p in local else remote[p]

@@ -776,16 +776,19 @@ class ClientShardedSerialAggregator(SerialAggregator):
             return
         super().add(key, value, weight)
 
-    def exchange(self, local_msgs: dict, n: int) -> list:
+    def exchange(self, local_msgs: dict, n: int, failed: bool = False) -> Optional[list]:
         """Every rank's client messages of this round, position by position:
         this rank's own as given, the others' rebuilt from what their ranks
         sent (tensors as RemoteRow stand-ins, 0-dim tensors and everything
-        else by value).  Collective."""
+        else by value).  Collective.  ``failed``: this rank's clients raised;
+        every rank then gets None (and raises), none is left waiting."""
         if self._solo:
-            return [None] * n
-        mine = {p: _skeleton(m, self._rank) for p, m in local_msgs.items()}
+            return None if failed else [None] * n
+        mine = None if failed else {p: _skeleton(m, self._rank) for p, m in local_msgs.items()}
         every = [None] * self._world
         dist.all_gather_object(every, mine, group=self._group)
+        if any(m is None for m in every):
+            return None
         dev = self._reduce_device()
         out = [None] * n
         for r, msgs in enumerate(every):

@@ -523,6 +523,21 @@ def _client_extras_worker(rank, world, port, outdir):
         alg.train(rounds=1)
         res["local_sgd_cloud"] = alg.get_server_storage().read("cloud_params").detach().tolist()
 
+        # (5) a client that raises on rank 1: every rank raises, none hangs
+        def failing(id, rounds, *a, _f=synth.send_to_server, **k):
+            if rank == 1 and rounds == 1:
+                raise ValueError("client failure on rank 1")
+            return _f(id, rounds, *a, **k)
+
+        alg = make(type("Failing", (synth,), {"send_to_server": staticmethod(failing)}))
+        try:
+            alg.train(rounds=S.ROUNDS)
+            res["failure"] = "none"
+        except ValueError as e:
+            res["failure"] = "own: " + str(e)
+        except RuntimeError as e:
+            res["failure"] = "other: " + str(e)
+
         # (3) FedDF keeps every client vector: refused on every rank
         feddf = S.make_algorithm(training.FedDF)
         alg = make(feddf)
@@ -552,6 +567,11 @@ def test_client_sharded_state_divergence_and_refusal():
         mp.start_processes(_client_extras_worker, args=(world, _free_port(), d), nprocs=world,
                            join=True, start_method="spawn")
         res = [json.load(open(os.path.join(d, f"extras_rank{r}.json"))) for r in range(world)]
+    assert res[1]["failure"] == "own: client failure on rank 1"
+    assert res[0]["failure"].startswith("other:")
+    for r in res[1:]:
+        r.pop("failure")
+    res[0].pop("failure")
     for r in res[1:]:
         assert r == res[0]
     sampled = res[0]["sampled"]
