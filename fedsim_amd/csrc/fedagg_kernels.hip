@@ -2481,13 +2481,26 @@ int pool_slide_cb(const fedagg_pool_args& a, int64_t plane) {
 // LRN of one element from its channel window, ATen's sequence
 // (torch/nn/functional.py local_response_norm): avg = s / size (exact as a
 // multiply when size is a power of two), d = (avg * alpha + k) ^ beta, v / d.
-// FAST: the power is exp2(beta * log2(b)) on the transcendental unit
-// (v_log_f32 / v_exp_f32) for a normal positive base b -- the LRN's case,
-// b >= k > 0 -- within a few ulps of powf at a small fraction of its
-// instructions (the pass is VALU-bound on powf otherwise); any other base
-// (lrn_fast_ok false), and every element when !FAST, takes powf.
-__device__ __forceinline__ bool lrn_fast_ok(float b) {
-  return b >= 1.17549435e-38f && b < 3.0e38f;
+// FAST: v * r with r = 1 / d = exp2(-beta * log2(b)) on the transcendental
+// unit (v_log_f32 / v_exp_f32), no powf and no IEEE division (the pass is
+// VALU-bound on them otherwise), within a few ulps of v / powf(b, beta);
+// taken when b is a normal positive number and |beta * log2(b)| < 126 (r and
+// 1 / r normal) -- the LRN's case, b >= k > 0.  Any other element
+// (lrn_fast_scale false), and every element when !FAST, is v / powf(b, beta).
+template <int SIZE>
+__device__ __forceinline__ float lrn_base(float sum, float size_f, float alpha, float k) {
+  float avg;
+  if constexpr (SIZE > 0 && (SIZE & (SIZE - 1)) == 0)
+    avg = sum * (1.0f / SIZE);
+  else
+    avg = sum / size_f;
+  return avg * alpha + k;
+}
+
+__device__ __forceinline__ bool lrn_fast_scale(float b, float nbeta, float& r) {
+  const float e = nbeta * __builtin_amdgcn_logf(b);
+  r = __builtin_amdgcn_exp2f(e);
+  return b >= 1.17549435e-38f && e > -126.0f && e < 126.0f;
 }
 
 // the rare powf of a fast LRN, out of line: the unrolled channel loops would
@@ -2497,18 +2510,13 @@ __device__ __noinline__ float lrn_powf(float b, float beta) { return powf(b, bet
 template <int SIZE, bool FAST>
 __device__ __forceinline__ float lrn_value(float v, float sum, float size_f, float alpha,
                                            float beta, float k) {
-  float avg;
-  if constexpr (SIZE > 0 && (SIZE & (SIZE - 1)) == 0)
-    avg = sum * (1.0f / SIZE);
-  else
-    avg = sum / size_f;
-  const float b = avg * alpha + k;
-  float d;
-  if constexpr (FAST)
-    d = lrn_fast_ok(b) ? __builtin_amdgcn_exp2f(beta * __builtin_amdgcn_logf(b)) : lrn_powf(b, beta);
-  else
-    d = powf(b, beta);
-  return v / d;
+  const float b = lrn_base<SIZE>(sum, size_f, alpha, k);
+  if constexpr (FAST) {
+    float r;
+    return lrn_fast_scale(b, -beta, r) ? v * r : v / lrn_powf(b, beta);
+  } else {
+    return v / powf(b, beta);
+  }
 }
 
 // Phase 2 of both variants: max-pool the CB padded planes in LDS into y.
@@ -2838,6 +2846,7 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 #pragma unroll
   for (int j = 0; j < CB; ++j) load(raw[j], g0 + LEAD + j);
   const float size_f = static_cast<float>(a.lrn_size);
+  const float nbeta = -a.lrn_beta;
   for (int c0 = g0; c0 < g1; c0 += CB) {
     const int cbn = g1 - c0 < CB ? g1 - c0 : CB;
 #pragma unroll
@@ -2855,21 +2864,43 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
           win[SW - 1][i] = raw[j][i];
           sq[SW - 1][i] = raw[j][i] * raw[j][i];
         }
+        // lrn_value<SIZE, true> of every position without a per-lane branch:
+        // the fast v * r everywhere, the powf division only when some lane
+        // of the wave needs it (one wave-uniform branch per channel)
+        float vv[NQ];
+        float bb[NQ];
+        bool slow = false;
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
-          const int q = threadIdx.x + 256 * i;
-          if (q < HpWp) {
-            float v = win[LO][i];
-            if constexpr (SIZE > 0) {
-              // ATen's sum from +0 in channel order: a square is never -0,
-              // so +0 + sq[0] is sq[0] and the chain starts there
-              float sum = sq[0][i];
+          vv[i] = win[LO][i];
+          if constexpr (SIZE > 0) {
+            // ATen's sum from +0 in channel order: a square is never -0,
+            // so +0 + sq[0] is sq[0] and the chain starts there
+            float sum = sq[0][i];
 #pragma unroll
-              for (int t = 1; t < SIZE; ++t) sum = sum + sq[t][i];
-              if (in[i]) v = lrn_value<SIZE, true>(v, sum, size_f, a.lrn_alpha, a.lrn_beta, a.lrn_k);
-            }
-            plane[j * HpWp + q] = v;
+            for (int t = 1; t < SIZE; ++t) sum = sum + sq[t][i];
+            bb[i] = lrn_base<SIZE>(sum, size_f, a.lrn_alpha, a.lrn_k);
+            float r;
+            const bool fast = lrn_fast_scale(bb[i], nbeta, r);
+            slow = slow || (in[i] && !fast);
+            vv[i] = in[i] ? vv[i] * r : vv[i];
           }
+        }
+        if constexpr (SIZE > 0) {
+          if (__builtin_expect(__ballot(slow) != 0, 0)) {
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+              float r;
+              if (in[i] && !lrn_fast_scale(bb[i], nbeta, r))
+                vv[i] = win[LO][i] / lrn_powf(bb[i], a.lrn_beta);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+          // positions 256 i + t of the first NQ - 1 groups are all inside
+          if (i + 1 < NQ || static_cast<int>(threadIdx.x) + 256 * i < HpWp)
+            plane[j * HpWp + threadIdx.x + 256 * i] = vv[i];
         }
       }
     }
