@@ -2205,25 +2205,48 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int row_lo = POOL ? 0 : (px0 - m_lo * OHW) / OW;
   const int row_hi = POOL ? Hp - 1 : (pend - (m_lo + last) * OHW) / OW + KS - 1;
   const int nrow = last * Hp + row_hi - row_lo + 1;  // rows this tile stages (<= nrows)
+  float* sDump = sX + CI * CP;  // one slot per thread: elements the tile does not need
+  float* sBias = sDump + kFlatThreads;
   for (int c = 0; c < CI; ++c)
     for (int q = t; q < nrow * Wp; q += kFlatThreads) sX[c * CP + q] = 0.f;
+  constexpr uint32_t kOut = 0x80000000u;  // past every descriptor: loads 0, stores dropped
+  // (slot, channel, row, column) of e = t + kFlatThreads * i, stepped by the
+  // mixed-radix digits of kFlatThreads (wave-uniform) instead of three
+  // divisions per element; an element the tile does not need loads 0 and is
+  // written to the thread's dump slot, so neither phase branches per lane
+  // A staged element sits in stacked padded row g = slot * Hp + h + pt; the
+  // tile needs rows row_lo .. last * Hp + row_hi, i.e. g - row_lo < nrow.
+  const int dW = kFlatThreads % W, qW = kFlatThreads / W;
+  const int dH = qW % H, qH = qW / H;
+  const int dC = qH % CI, dS = qH / CI;
+  int ew = t % W, eh = (t / W) % H, ec = (t / W / H) % CI, es = t / W / H / CI;
+  const int g0 = pt - row_lo;
+  (void)xtot;  // rows past the last image are past row_hi of the last slot
   float rx[XM];
   int lidx[XM];
 #pragma unroll
   for (int i = 0; i < XM; ++i) {
     const int e = t + kFlatThreads * i;
-    const int sc = e / HW;  // slot * CI + channel
-    const int slot = sc / CI;
-    const int hw = e - sc * HW;
-    const int h = hw / W;
-    const int prow = h + pt;
-    const bool need = e < xtot && slot <= last && (slot > 0 || prow >= row_lo) &&
-                      (slot < last || prow <= row_hi);
-    lidx[i] = need ? ((sc - slot * CI) * nrows + slot * Hp + prow - row_lo) * Wp + (hw - h * W) + pl
-                   : -1;
-    rx[i] = need ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                          xres, static_cast<int>(e * 4u + x_tile4), 0, 0))
-                 : 0.f;
+    const int gr = __mul24(es, Hp) + eh + g0;  // staged row, from row_lo
+    const bool need = static_cast<unsigned>(gr) < static_cast<unsigned>(nrow);
+    lidx[i] = need ? __mul24(ec, CP) + __mul24(gr, Wp) + ew + pl : CI * CP + t;
+    rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                          xres, static_cast<int>(need ? e * 4u + x_tile4 : kOut), 0, 0));
+    ew += dW;
+    int cy = ew >= W;
+    ew -= cy ? W : 0;
+    eh += dH + cy;
+    cy = eh >= H;
+    eh -= cy ? H : 0;
+    ec += dC + cy;
+    cy = ec >= CI;
+    ec -= cy ? CI : 0;
+    es += dS + cy;
+  }
+  // this tile's biases (0 past OC, or without a bias), read back per output channel
+  if (t < kTC_OC) {
+    const int oc = oc0 + t;
+    sBias[t] = (b_off >= 0 && oc < OC) ? params[k * params_kstride + b_off + oc] : 0.f;
   }
   // weights: thread t owns output channel oc0 + t / 4, columns t % 4 + 4 i
   // (columns past R, and rows past OC, are zero)
@@ -2238,12 +2261,12 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
                              : 0.f;
   __syncthreads();  // halo zeroes before the planes land
 #pragma unroll
-  for (int i = 0; i < XM; ++i)
-    if (lidx[i] >= 0) sX[lidx[i]] = rx[i];
+  for (int i = 0; i < XM; ++i) sX[lidx[i]] = rx[i];
 #pragma unroll
   for (int i = 0; i < WPT; ++i)
     if (t < 256 && wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
   __syncthreads();
+  (void)sDump;
   const int col = lane & 31;
   const int kk = lane >> 5;
   const float* pa = sW + col * RW + kk;
@@ -2307,74 +2330,77 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv[1], acc[1][1], 0, 0, 0);
     }
   }
-  // epilogue: each bias value loaded once for both pixel groups
-  const float* bk = b_off >= 0 ? params + k * params_kstride + b_off : nullptr;
-  if constexpr (POOL) {
-    // a quad of lanes holds one window's members in order; all four lanes of
-    // a quad are in or out of the launch together (NPX is a multiple of 4)
-    float* yq[NPG];
-    bool pin[NPG], inside[NPG];
-#pragma unroll
-    for (int b = 0; b < NPG; ++b) {
-      const int p = px0 + wave * 32 * NPG + b * 32 + col;
-      pin[b] = p < NPX;
-      const int q = (pin[b] ? p : 0) >> 2, d = p & 3;
-      const int m = q / PHW;
-      const int ij = q - m * PHW;
-      const int i = ij / PW;
-      const int oh = 2 * i - ppad + (d >> 1);
-      const int ow = 2 * (ij - i * PW) - ppad + (d & 1);
-      inside[b] = oh >= 0 && oh < OH && ow >= 0 && ow < OW;
-      yq[b] = y + (k * s.M + m) * s.OC * PHW + ij;
-    }
-    const bool leader = (col & 3) == 0;
-#pragma unroll
-    for (int a = 0; a < (HALF ? 1 : 2); ++a) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
-        if (oc >= OC) continue;  // uniform over each 32-lane half, so over quads
-        const float bias = bk ? bk[oc] : 0.f;
-#pragma unroll
-        for (int b = 0; b < NPG; ++b) {
-          if (!pin[b]) continue;
-          float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias;
-          if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
-          if (!inside[b]) v = -__builtin_huge_valf();
-          v = pool_dpp_max<0xB1>(v);  // members (0, 1) and (2, 3): quad_perm [1, 0, 3, 2]
-          v = pool_dpp_max<0x4E>(v);  // then (01, 23): quad_perm [2, 3, 0, 1]
-          if (leader) yq[b][int64_t(oc) * PHW] = v;
-        }
-      }
-    }
-    return;
-  }
-  float* yp[NPG];
-  bool pin[NPG];
+  // epilogue: buffer stores into this teacher's output, the lane's pixel in
+  // the VGPR offset (kOut: a pixel past the launch, a channel past OC, a
+  // non-leader lane of a pooled window -- the store is dropped), the output
+  // channel's plane in the scalar offset; the bias from LDS.  No per-lane
+  // branch, no 64-bit address per store.
+  const int PLANE = POOL ? PHW : OHW;  // per output channel
+  const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
+      y + k * s.M * s.OC * PLANE, static_cast<short>(0), static_cast<int>(s.M * s.OC * PLANE * 4),
+      0x00020000);
+  uint32_t yoff[NPG];
+  bool inside[NPG];
 #pragma unroll
   for (int b = 0; b < NPG; ++b) {
     const int p = px0 + wave * 32 * NPG + b * 32 + col;
-    pin[b] = p < NPX;
-    const int pc = pin[b] ? p : 0;
-    const int m = pc / OHW;
-    yp[b] = y + (k * s.M + m) * s.OC * OHW + (pc - m * OHW);
+    const bool pin = p < NPX;
+    const int pc = pin ? p : 0;
+    int m, pix;
+    if constexpr (POOL) {
+      // a quad of lanes holds one window's members in order; all four lanes
+      // of a quad are in or out of the launch together (NPX is a multiple of 4)
+      const int q = pc >> 2, d = pc & 3;
+      m = q / PHW;
+      pix = q - m * PHW;
+      const int i = pix / PW;
+      const int oh = 2 * i - ppad + (d >> 1);
+      const int ow = 2 * (pix - i * PW) - ppad + (d & 1);
+      inside[b] = oh >= 0 && oh < OH && ow >= 0 && ow < OW;
+    } else {
+      m = pc / OHW;
+      pix = pc - m * OHW;
+      inside[b] = true;
+    }
+    const bool store = pin && (!POOL || (col & 3) == 0);
+    yoff[b] = store ? static_cast<uint32_t>((m * OC + 4 * kk) * PLANE + pix) * 4u : kOut;
   }
+  // FULL: every channel of the tile exists (the common case, no channel test)
+  auto epilogue = [&](auto full) {
+    constexpr bool FULL = decltype(full)::value;
 #pragma unroll
-  for (int a = 0; a < (HALF ? 1 : 2); ++a) {
+    for (int a = 0; a < (HALF ? 1 : 2); ++a) {
+      float bias[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int oc = oc0 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * kk;
-      if (oc >= OC) continue;
-      const float bias = bk ? bk[oc] : 0.f;
+      for (int e = 0; e < 16; ++e) {
+        if ((e & 3) == 0) {  // read four at a time: one LDS wait per 4 channels
 #pragma unroll
-      for (int b = 0; b < NPG; ++b) {
-        if (!pin[b]) continue;
-        float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias;
-        if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
-        yp[b][int64_t(oc) * OHW] = v;
+          for (int j = 0; j < 4; ++j) bias[e + j] = sBias[a * 32 + j + 2 * e + 4 * kk];
+        }
+        const int ocr = a * 32 + (e & 3) + 8 * (e >> 2);  // + 4 kk: this lane's channel
+        if (!FULL && oc0 + ocr >= OC) continue;  // wave-uniform: both halves past OC
+        const bool cok = FULL || oc0 + ocr + 4 * kk < OC;
+        const uint32_t soff = static_cast<uint32_t>((oc0 + ocr) * PLANE) * 4u;
+#pragma unroll
+        for (int b = 0; b < NPG; ++b) {
+          float v = (HALF ? acc[b >> 1][b & 1][e] : acc[a][b & 1][e]) + bias[e];
+          if (relu) v = v < 0.f ? 0.f : v;  // torch.relu: keeps NaN and -0
+          if constexpr (POOL) {
+            if (!inside[b]) v = -__builtin_huge_valf();
+            v = pool_dpp_max<0xB1>(v);  // members (0, 1) and (2, 3): quad_perm [1, 0, 3, 2]
+            v = pool_dpp_max<0x4E>(v);  // then (01, 23): quad_perm [2, 3, 0, 1]
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), yres,
+                                                static_cast<int>(cok ? yoff[b] : kOut),
+                                                static_cast<int>(soff), 0);
+        }
       }
     }
-  }
+  };
+  if (oc0 + (HALF ? 32 : kTC_OC) <= OC)
+    epilogue(std::true_type{});
+  else
+    epilogue(std::false_type{});
 }
 
 // Launch plan of k_teacher_conv2d_lds for a shape, or false (the gather
@@ -2405,7 +2431,9 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
     int64_t fslot = (per_tile - 2) / per_img + 2;
     if (fslot > s.M) fslot = s.M;
     const int64_t xall = s.C * fslot * HW;
-    if (xall <= 16 * kFlatThreads) {
+    // one teacher's output is stored through a buffer descriptor (31-bit offsets)
+    const bool y_fits = s.M * s.OC * per_img * 4 < (int64_t(1) << 31);
+    if (xall <= 16 * kFlatThreads && y_fits) {
       const int64_t rw = (s.C * ks * ks + 1) / 2 * 2 + 1;
       // rows a tile reads: its output rows (a run of tpx pixels meets at most
       // ceil((tpx - 1) / OW) + 1 of them; image boundaries are row
@@ -2420,7 +2448,9 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
       p->xm = xall <= 8 * kFlatThreads ? 8 : 16;
       p->nslot = static_cast<int>(fslot);
       p->nrows = static_cast<int>(nrows);
-      p->lds = static_cast<size_t>(kTC_OC * rw + s.C * nrows * Wp) * sizeof(float);
+      // weights, the staged rows, one dump slot per thread, the tile's biases
+      p->lds = static_cast<size_t>(kTC_OC * rw + s.C * nrows * Wp + kFlatThreads + kTC_OC) *
+               sizeof(float);
       if (p->lds <= 64 * 1024) return true;
     }
   }

@@ -20,7 +20,9 @@ def linear_stub(x, slab, w_off, b_off, in_f, out_f, shared, relu=False):
     K = slab.shape[0]
     W = slab[:, w_off:w_off + in_f * out_f].view(K, out_f, in_f)
     xs = x.reshape(1 if shared else K, -1, in_f).expand(K, -1, -1)
-    y = torch.einsum("kmi,koi->kmo", xs, W)
+    # one GEMM per teacher: a batched einsum's CPU blocking (and so its
+    # rounding) can depend on K, which the teacher-chunk test varies
+    y = torch.stack([xs[k] @ W[k].t() for k in range(K)])
     if b_off >= 0:
         y = y + slab[:, b_off:b_off + out_f].view(K, 1, out_f)
     return torch.relu(y) if relu else y
@@ -239,7 +241,10 @@ def test_replay_in_teacher_chunks():
     got = prog(x)
     assert prog.K == K and prog.slab is slab
     assert prog.conv_launches == 2 * 3  # two convs x three passes (3, 3, 1 teachers)
-    torch.testing.assert_close(got, whole, rtol=0, atol=0)
+    # not bit for bit: the vmap'd segments and torch's CPU pooling may block
+    # their loops by the batch (K x M), which differs between the passes on
+    # some CPUs (the GPU box's EPYC); a mis-stitched chunk is off by O(1)
+    torch.testing.assert_close(got, whole, rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("name,kw,shape", [
