@@ -603,6 +603,12 @@ class _ClientShardEntry(_TensorEntry):
         if tuple(value.shape) != self.shape:
             raise ValueError(
                 f"tensor of shape {tuple(value.shape)} added to a key aggregating {self.shape}")
+        if self.sum is not None:
+            # the rows were combined across ranks by a get / get_sum: a later
+            # row would have to be chained onto that sum on its owner, which
+            # this round protocol does not do -- refuse rather than drop it
+            raise RuntimeError("add after get / get_sum of a key in a client-sharded round "
+                               "is not supported (pop the key first)")
         if isinstance(value, RemoteRow):
             self._owner(value.owner)
         else:

@@ -249,6 +249,28 @@ def test_round_driver_shard_over_option():
         ClientShardedSerialAggregator(mode="tree")
 
 
+def test_client_sharded_add_after_get_is_refused():
+    """Solo (no process group): a get combines the key's rows; a later add
+    would not reach that sum, so it raises instead of being dropped."""
+    import numpy as np
+
+    from fedsim_amd.sharding import ClientShardedSerialAggregator
+    from shard_oracle import ChainOracleEntry, oracle_step
+
+    from oracle import ref
+
+    agg = ClientShardedSerialAggregator(entry_factory=ChainOracleEntry, step_impl=oracle_step)
+    rows = [torch.randn(33) for _ in range(3)]
+    for k, r in enumerate(rows[:2]):
+        agg.add("local_params", r, 10 + k)
+    got = agg.get("local_params")
+    want = ref.reduce(np.stack([r.numpy() for r in rows[:2]]), [10, 11], W=21)
+    np.testing.assert_array_equal(got.numpy().view(np.uint32), want.view(np.uint32))
+    with pytest.raises(RuntimeError):
+        agg.add("local_params", rows[2], 12)
+    assert torch.equal(agg.pop("local_params"), got)
+
+
 def _api_worker(rank, world, port, outdir):
     """Every SerialAggregator call on a parameter-sharded key, including
     shards that are empty (P < 64 * world), against the one-process oracle."""
