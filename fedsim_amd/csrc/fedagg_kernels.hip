@@ -2458,10 +2458,14 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
 #ifndef FEDAGG_CONV_CC2_XM16  // chunks of 2 channels where 4 would need 16 staging registers
 #define FEDAGG_CONV_CC2_XM16 1  // (SimpleCNN conv2, 32 ch at 14x14: whole teacher batch at
 #endif                          // K=1000 14.55 -> 13.97 ms, profiles/r02xa; 0 for A/B builds)
+#ifndef FEDAGG_CONV_XM12  // chunks of 4 channels with 12 staging registers where 8 do not
+#define FEDAGG_CONV_XM12 0  // suffice (A/B build knob)
+#endif
   int cc = s.C >= 4 ? 4 : 2;
-  if (FEDAGG_CONV_CC2_XM16 && cc == 4 && cc * nslot * HW > 8 * 256) cc = 2;
+  if (FEDAGG_CONV_CC2_XM16 && cc == 4 && cc * nslot * HW > (FEDAGG_CONV_XM12 ? 12 : 8) * 256)
+    cc = 2;
   const int64_t xtot = cc * nslot * HW;
-  const int xm = xtot <= 8 * 256 ? 8 : 16;
+  const int xm = xtot <= 8 * 256 ? 8 : (FEDAGG_CONV_XM12 && xtot <= 12 * 256) ? 12 : 16;
   if (xtot > xm * 256) return false;
   if (nslot * cc * Hp * Wp >= (int64_t(1) << kTC_XPK_LDS)) return false;
   if (nslot * s.C * HW + cc * HW >= (int64_t(1) << kTC_XPK_GLB)) return false;
@@ -3267,13 +3271,17 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
         }
       } else if (plan.ks == 5) {
         if (plan.cc == 4) {
-          if (plan.xm == 8) FEDAGG_CONV_LDS(5, 4, 8); else FEDAGG_CONV_LDS(5, 4, 16);
+          if (plan.xm == 8) FEDAGG_CONV_LDS(5, 4, 8);
+          else if (plan.xm == 12) FEDAGG_CONV_LDS(5, 4, 12);
+          else FEDAGG_CONV_LDS(5, 4, 16);
         } else {
           if (plan.xm == 8) FEDAGG_CONV_LDS(5, 2, 8); else FEDAGG_CONV_LDS(5, 2, 16);
         }
       } else {
         if (plan.cc == 4) {
-          if (plan.xm == 8) FEDAGG_CONV_LDS(3, 4, 8); else FEDAGG_CONV_LDS(3, 4, 16);
+          if (plan.xm == 8) FEDAGG_CONV_LDS(3, 4, 8);
+          else if (plan.xm == 12) FEDAGG_CONV_LDS(3, 4, 12);
+          else FEDAGG_CONV_LDS(3, 4, 16);
         } else {
           if (plan.xm == 8) FEDAGG_CONV_LDS(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
         }
