@@ -1,8 +1,8 @@
 #!/bin/bash
 # End-of-round evidence on the final round-3 tree: GPU suite + smoke, the
 # bench line and its rocprof kernel stats, the headline kernel's PMC traffic
-# (FETCH_SIZE / WRITE_SIZE passes + calibration), config-4 / config-5 modes,
-# the plugin round, ingest and the FedDF teacher bench.  Large traces stay in
+# (FETCH_SIZE / WRITE_SIZE passes + calibration); the config-4 / config-5
+# modes, plugin round, ingest and FedDF bench are tools/gpu_r03_evidence_b.sh.  Large traces stay in
 # /tmp on the box; only summaries land under gpurun_out/.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -16,7 +16,7 @@ pmc() {  # pmc <counter> <dir> <cmd...>
   timeout -s KILL 300 rocprofv3 --pmc "$c" --output-format csv -d "$OUT/$d" -o "$d" -- "$@" \
     > "$OUT/$d.log" 2>&1
 }
-timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
 && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
 && timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
 && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/r03prof -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.log" 2>&1 \
@@ -29,12 +29,7 @@ timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeou
      --layout blocked4096 --step fused --kernel-match "k_reduce_narrow<8, 2," \
      --label "k_reduce_narrow<U=8, VW=2>" --width 2 \
      --calib-fetch "$OUT/calib_fetch" --calib-write "$OUT/calib_write" \
-     --out "$OUT/pmc_traffic.json" \
-&& timeout -k 10 300 python bench.py --mode strong --no-cpu-baseline > "$OUT/bench_strong.json" 2> "$OUT/bench_strong.err" \
-&& timeout -k 10 300 python bench.py --mode allreduce --no-cpu-baseline > "$OUT/bench_allreduce.json" 2> "$OUT/bench_allreduce.err" \
-&& timeout -k 10 600 python tools/bench_plugin_round.py --headline --reps 3 > "$OUT/plugin_round.jsonl" 2> "$OUT/plugin_round.err" \
-&& timeout -k 10 300 python tools/bench_ingest.py > "$OUT/ingest.json" 2> "$OUT/ingest.err" \
-&& timeout -k 10 600 python tools/bench_feddf_teachers.py > "$OUT/feddf_teachers.jsonl" 2> "$OUT/feddf_teachers.err"
+     --out "$OUT/pmc_traffic.json"
 rc=$?
 echo "exit $rc"
 exit $rc
