@@ -2197,7 +2197,6 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   // channel (the host's bound for any tile), so the workgroup's LDS holds
   // only those rows and more workgroups fit on a CU.
   const int CP = nrows * Wp;  // channel pitch in sX
-  const int xtot = nslot * CI * HW;
   const int pend = (px0 + TPX < NPX ? px0 + TPX : NPX) - 1;
   // slot of the tile's last image; the padded rows its pixels read (POOL:
   // whole images, a window's rows straddle the tile's first / last row)
@@ -2205,8 +2204,9 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int row_lo = POOL ? 0 : (px0 - m_lo * OHW) / OW;
   const int row_hi = POOL ? Hp - 1 : (pend - (m_lo + last) * OHW) / OW + KS - 1;
   const int nrow = last * Hp + row_hi - row_lo + 1;  // rows this tile stages (<= nrows)
-  float* sDump = sX + CI * CP;  // one slot per thread: elements the tile does not need
-  float* sBias = sDump + kFlatThreads;
+  // after the staged rows: one dump slot per thread (sX[CI * CP + t], for
+  // elements the tile does not need), then the tile's biases
+  float* sBias = sX + CI * CP + kFlatThreads;
   for (int c = 0; c < CI; ++c)
     for (int q = t; q < nrow * Wp; q += kFlatThreads) sX[c * CP + q] = 0.f;
   constexpr uint32_t kOut = 0x80000000u;  // past every descriptor: loads 0, stores dropped
@@ -2221,7 +2221,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int dC = qH % CI, dS = qH / CI;
   int ew = t % W, eh = (t / W) % H, ec = (t / W / H) % CI, es = t / W / H / CI;
   const int g0 = pt - row_lo;
-  (void)xtot;  // rows past the last image are past row_hi of the last slot
+  // (an element of an image past the tile's last is past row_hi of the last slot)
   float rx[XM];
   int lidx[XM];
 #pragma unroll
@@ -2266,7 +2266,6 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   for (int i = 0; i < WPT; ++i)
     if (t < 256 && wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
   __syncthreads();
-  (void)sDump;
   const int col = lane & 31;
   const int kk = lane >> 5;
   const float* pa = sW + col * RW + kk;
