@@ -1476,6 +1476,24 @@ constexpr int kTL_PAD = 1;
 #ifndef FEDAGG_TL_PAD_KB  // LDS reserved per workgroup of a wide layer: 4 per CU (A/B: 0 = none)
 #define FEDAGG_TL_PAD_KB 20
 #endif
+
+// XCD-aware order of a 1-D grid of teacher tiles (the 1-D form of
+// conv_tile_order below): launch index L runs on XCD L % 8, so in plain order
+// the n_tiles x m_tiles tiles of one teacher land on up to eight XCDs and each
+// fetches the teacher's input rows into its own L2 (SimpleCNN's fc: 8 output
+// tiles, a 0.8 MB input per teacher).  Renumbered, each XCD walks one
+// contiguous range of tiles, so a teacher's tiles share one L2.  Bijective;
+// placement only changes speed, never results.
+#ifndef FEDAGG_LINEAR_XCD_ORDER  // 0: plain dispatch order (A/B builds)
+#define FEDAGG_LINEAR_XCD_ORDER 1
+#endif
+__device__ __forceinline__ uint32_t xcd_tile_1d() {
+  const uint32_t L = blockIdx.x;
+  if (!FEDAGG_LINEAR_XCD_ORDER) return L;
+  const uint32_t n = gridDim.x, xcd = L & 7u, slot = L >> 3, q = n >> 3, r = n & 7u;
+  return slot + (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q);
+}
+
 __global__ __launch_bounds__(256)
 #if FEDAGG_TL_WPE
 __attribute__((amdgpu_waves_per_eu(FEDAGG_TL_WPE, FEDAGG_TL_WPE)))
@@ -1486,7 +1504,7 @@ void k_teacher_linear(
     float* __restrict__ y, int64_t n_tiles, int64_t m_tiles, int relu) {
   __shared__ float sx[kTL_M][kTL_K + kTL_PAD];
   __shared__ float sw[kTL_N][kTL_K + kTL_PAD];
-  const int64_t tile = blockIdx.x;
+  const int64_t tile = xcd_tile_1d();
   const int64_t k = tile / (n_tiles * m_tiles);
   const int64_t rem = tile - k * n_tiles * m_tiles;
   const int64_t m0 = (rem / n_tiles) * kTL_M;
@@ -1613,7 +1631,7 @@ __global__ __launch_bounds__(256) void k_teacher_linear_buf(
   __shared__ float sx[kTL_M][kTL_K + kTL_PAD];
   __shared__ float sw[kTL_N][kTL_K + kTL_PAD];
   const int tiles = n_tiles * m_tiles;
-  const int tile = blockIdx.x;
+  const int tile = __builtin_amdgcn_readfirstlane(static_cast<int>(xcd_tile_1d()));
   const int k = tile / tiles;
   const int rem = tile - k * tiles;
   const int m0 = (rem / n_tiles) * kTL_M;
