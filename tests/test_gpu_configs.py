@@ -270,11 +270,13 @@ def test_configs_1_to_3_cli_defaults_bitwise_vs_reference_round_loop(rid, device
     assert {k: float(v) for k, v in scores.items()} == run["scores"]
 
 
-def _gpu_slab_client(record, cols):
+def _gpu_slab_client(record, cols, slab_row=True):
     """A client that trains on the GPU, as local_updates.sgd_update hands its
     update over: its model's parameters become views of one fresh device
     vector (cloud + a seeded N(0, 1e-3) delta), which vectorize_module packs
-    into the round's reserved slab row.  Records (vector[cols], weight)."""
+    into the round's reserved slab row (``slab_row=False``: a fresh
+    ``torch.cat`` vector instead, the reference client's own hand-over, which
+    the aggregator borrows in place).  Records (vector[cols], weight)."""
     from torch.nn.utils import parameters_to_vector, vector_to_parameters
 
     from fedsim_amd.utils import vectorize_module
@@ -288,8 +290,10 @@ def _gpu_slab_client(record, cols):
         g = torch.Generator(device=base.device).manual_seed(1_000_003 * rounds + id)
         local = base + torch.empty_like(base).normal_(0.0, 1e-3, generator=g)
         vector_to_parameters(local, model.parameters())
-        row = reserve_round_row("local_params", model)
-        assert row is not None and row.in_slab
+        row = None
+        if slab_row:
+            row = reserve_round_row("local_params", model)
+            assert row is not None and row.in_slab
         n = len(datasets[train_split_name])
         record.append((local[cols], n))
         return dict(local_params=vectorize_module(model, out=row), num_steps=max(1, n // 32),
@@ -299,11 +303,13 @@ def _gpu_slab_client(record, cols):
     return send_to_server
 
 
+@pytest.mark.parametrize("slab_row", [True, False], ids=["slab_rows", "borrowed"])
 @pytest.mark.parametrize("algo", ["FedAvg", "AdaBest"])
-def test_configs_2_3_full_participation_slab_rows_1000x1_085_668(algo):
+def test_configs_2_3_full_participation_1000x1_085_668(algo, slab_row):
     """(e) -c 1.0: K = 1000 clients x SimpleCNN2's 1 085 668 parameters, one
-    round through the round driver with every client in a slab row; the
-    server step is the split pass at this size."""
+    round through the round driver with every client in a slab row, or
+    handing over a fresh vector that the aggregator borrows (the row-pointer
+    kernels); the server step is the split pass at this size."""
     from fedsim_amd import models, ops
     from fedsim_amd.distributed.centralized import training
 
@@ -313,7 +319,7 @@ def test_configs_2_3_full_participation_slab_rows_1000x1_085_668(algo):
     c = torch.from_numpy(cols).to(DEV)
     record = []
     base = getattr(training, algo)
-    cls = type("Gpu" + algo, (base,), {"send_to_server": _gpu_slab_client(record, c)})
+    cls = type("Gpu" + algo, (base,), {"send_to_server": _gpu_slab_client(record, c, slab_row)})
     akw = dict(mu=0.01, beta=0.6) if algo == "AdaBest" else {}
     random.seed(S.RANDOM_SEED)
     torch.manual_seed(S.TORCH_SEED)
@@ -326,15 +332,22 @@ def test_configs_2_3_full_participation_slab_rows_1000x1_085_668(algo):
     cloud0 = st.read("cloud_params").detach()[c].cpu().numpy()
     prev0 = st.read("avg_params")[c].cpu().numpy() if algo == "AdaBest" else None
     assert st.read("cloud_params").numel() == P
-    split = []
+    split, borrowed = [], []
+
+    def spy(*a, **k):
+        borrowed.append(bool(k.get("borrowed", False)))
+        split.append(not orig(*a, **k))
+        return orig(*a, **k)
+
     orig = ops.fuse_step_pays
-    ops.fuse_step_pays = lambda *a, **k: split.append(not orig(*a, **k)) or orig(*a, **k)
+    ops.fuse_step_pays = spy
     try:
         alg.train(rounds=0)  # one round
     finally:
         ops.fuse_step_pays = orig
     assert len(record) == n_clients
     assert split and all(split)  # the split pop + step at this size
+    assert borrowed == [not slab_row]  # rows read in the slab, or where the clients left them
     sub = torch.stack([v for v, _ in record]).cpu().numpy()  # [K, n] in arrival order
     w = [n for _, n in record] if algo == "FedAvg" else [1] * n_clients
     avg = ref.reduce(sub, w, W=sum(w))
