@@ -2222,34 +2222,40 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
   const int row_lo = POOL ? 0 : (px0 - m_lo * OHW) / OW;
   const int row_hi = POOL ? Hp - 1 : (pend - (m_lo + last) * OHW) / OW + KS - 1;
   const int nrow = last * Hp + row_hi - row_lo + 1;  // rows this tile stages (<= nrows)
-  // after the staged rows: one dump slot per thread (sX[CI * CP + t], for
-  // elements the tile does not need), then the tile's biases
-  float* sBias = sX + CI * CP + kFlatThreads;
+  // after the staged rows: four dump slots per thread (sX[CI * CP + 4 t ..],
+  // for elements the tile does not need), then the tile's biases
+  float* sBias = sX + CI * CP + 4 * kFlatThreads;
   for (int c = 0; c < CI; ++c)
     for (int q = t; q < nrow * Wp; q += kFlatThreads) sX[c * CP + q] = 0.f;
   constexpr uint32_t kOut = 0x80000000u;  // past every descriptor: loads 0, stores dropped
-  // (slot, channel, row, column) of e = t + kFlatThreads * i, stepped by the
-  // mixed-radix digits of kFlatThreads (wave-uniform) instead of three
-  // divisions per element; an element the tile does not need loads 0 and is
-  // written to the thread's dump slot, so neither phase branches per lane
+  // (slot, channel, row, column) of each staged element (group), stepped by
+  // the mixed-radix digits of the per-load step (wave-uniform) instead of
+  // three divisions per element; one the tile does not need loads 0 and is
+  // written to the thread's dump slots, so neither phase branches per lane.
   // A staged element sits in stacked padded row g = slot * Hp + h + pt; the
-  // tile needs rows row_lo .. last * Hp + row_hi, i.e. g - row_lo < nrow.
-  const int dW = kFlatThreads % W, qW = kFlatThreads / W;
+  // tile needs rows row_lo .. last * Hp + row_hi, i.e. g - row_lo < nrow
+  // (an element of an image past the tile's last is past row_hi of the last slot).
+  const int g0 = pt - row_lo;
+  // V4 (rows a multiple of 4 wide, 16-B aligned input: the reference models'
+  // 24- and 28-wide images): groups of 4 elements of one row per 16-byte
+  // load, stepped by the digits of 4 x kFlatThreads; else single elements
+  const bool v4 = (W & 3) == 0 && (x_kstride & 3) == 0 &&
+                  (reinterpret_cast<uintptr_t>(x) & 15) == 0;  // wave-uniform
+  const int NE = v4 ? 4 : 1;  // elements per load
+  const int step = NE * kFlatThreads;
+  const int dW = step % W, qW = step / W;
   const int dH = qW % H, qH = qW / H;
   const int dC = qH % CI, dS = qH / CI;
-  int ew = t % W, eh = (t / W) % H, ec = (t / W / H) % CI, es = t / W / H / CI;
-  const int g0 = pt - row_lo;
-  // (an element of an image past the tile's last is past row_hi of the last slot)
+  const int e0 = NE * t;
+  int ew = e0 % W, eh = (e0 / W) % H, ec = (e0 / W / H) % CI, es = e0 / W / H / CI;
   float rx[XM];
   int lidx[XM];
-#pragma unroll
-  for (int i = 0; i < XM; ++i) {
-    const int e = t + kFlatThreads * i;
+  auto locate = [&](int i) {  // LDS index (or the dump) and load offset of load i
+    const int e = e0 + step * i;
     const int gr = __mul24(es, Hp) + eh + g0;  // staged row, from row_lo
     const bool need = static_cast<unsigned>(gr) < static_cast<unsigned>(nrow);
-    lidx[i] = need ? __mul24(ec, CP) + __mul24(gr, Wp) + ew + pl : CI * CP + t;
-    rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                          xres, static_cast<int>(need ? e * 4u + x_tile4 : kOut), 0, 0));
+    lidx[i] = need ? __mul24(ec, CP) + __mul24(gr, Wp) + ew + pl : CI * CP + NE * t;
+    const uint32_t off = need ? e * 4u + x_tile4 : kOut;
     ew += dW;
     int cy = ew >= W;
     ew -= cy ? W : 0;
@@ -2260,6 +2266,20 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
     cy = ec >= CI;
     ec -= cy ? CI : 0;
     es += dS + cy;
+    return static_cast<int>(off);
+  };
+  if (v4) {
+#pragma unroll
+    for (int i = 0; i < XM / 4; ++i) {
+      const f32x4 v = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(xres, locate(i), 0, 0));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rx[4 * i + q] = v[q];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < XM; ++i)
+      rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xres, locate(i), 0, 0));
   }
   // this tile's biases (0 past OC, or without a bias), read back per output channel
   if (t < kTC_OC) {
@@ -2278,8 +2298,15 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FE
                                                      wres, static_cast<int>(wg4 + 16u * i), 0, 0))
                              : 0.f;
   __syncthreads();  // halo zeroes before the planes land
+  if (v4) {
 #pragma unroll
-  for (int i = 0; i < XM; ++i) sX[lidx[i]] = rx[i];
+    for (int i = 0; i < XM / 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sX[lidx[i] + q] = rx[4 * i + q];
+  } else {
+#pragma unroll
+    for (int i = 0; i < XM; ++i) sX[lidx[i]] = rx[i];
+  }
 #pragma unroll
   for (int i = 0; i < WPT; ++i)
     if (t < 256 && wq + 4 * i < 2 * RP) sW[wl + 4 * i] = rw[i];
@@ -2465,8 +2492,8 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
       p->xm = xall <= 8 * kFlatThreads ? 8 : 16;
       p->nslot = static_cast<int>(fslot);
       p->nrows = static_cast<int>(nrows);
-      // weights, the staged rows, one dump slot per thread, the tile's biases
-      p->lds = static_cast<size_t>(kTC_OC * rw + s.C * nrows * Wp + kFlatThreads + kTC_OC) *
+      // weights, the staged rows, four dump slots per thread, the tile's biases
+      p->lds = static_cast<size_t>(kTC_OC * rw + s.C * nrows * Wp + 4 * kFlatThreads + kTC_OC) *
                sizeof(float);
       if (p->lds <= 64 * 1024) return true;
     }
