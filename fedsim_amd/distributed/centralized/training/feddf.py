@@ -28,7 +28,8 @@ MI355X-first differences:
 * Parity is normwise, not bitwise, on this path: the matrix-core layers sum
   each output as one fmaf chain (not the CPU GEMM's order) and the LRN power
   is exp2/log2, a few ulps from powf.  The replay is checked against the
-  whole-model ``vmap`` on its first batch (normwise 1e-4) and pinned to the
+  whole-model ``vmap`` on its first batch (normwise 1e-4; on the first and
+  last 32 teachers when there are more than 64) and pinned to the
   reference's own SimpleCNN2 / SimpleCNN FedDF rounds
   (tests/golden/feddf_cnn.*, tests/test_gpu_feddf_cnn.py).
 * Whenever the replay is not used -- the forward does not trace, a kernel
@@ -68,6 +69,13 @@ from .fedavg import FedAvg
 from .utils import serial_aggregation
 
 _TEACHER_CHUNK = 64  # teachers per batched forward (bounds activation memory)
+# teachers the replay is checked on against the whole-model vmap (first
+# batch of a round): all of them up to this many, else the first and the last
+# half of it -- the replay runs every teacher through the same kernels, and
+# the ends cover the first and last teacher chunk and slab rows; the check
+# then costs a 64-teacher vmap instead of a K-teacher one (131 ms at K=1000
+# for SimpleCNN2, more than five replayed batches)
+_CHECK_TEACHERS = 64
 
 
 def _in_order(loader) -> bool:
@@ -156,12 +164,20 @@ class TeacherEnsemble(object):
     def _forward(self, flat, x):
         return functional_call(self.model, vector_to_named_parameters_like(flat, self.named), (x,))
 
-    def _vmap_logits(self, x):
+    def _vmap_logits(self, x, rows=None):
+        slab = self.slab if rows is None else self.slab[rows]
         chunks = []
-        for k0 in range(0, self.K, _TEACHER_CHUNK):
-            part = self.slab[k0:k0 + _TEACHER_CHUNK]
+        for k0 in range(0, slab.shape[0], _TEACHER_CHUNK):
+            part = slab[k0:k0 + _TEACHER_CHUNK]
             chunks.append(torch.vmap(self._forward, in_dims=(0, None))(part, x))
         return torch.cat(chunks) if len(chunks) > 1 else chunks[0]
+
+    def _check_rows(self):
+        """The teachers the first-batch check compares (None: all)."""
+        if self.K <= _CHECK_TEACHERS:
+            return None
+        h = _CHECK_TEACHERS // 2
+        return torch.cat([torch.arange(h), torch.arange(self.K - h, self.K)]).to(self.slab.device)
 
     def teacher_logits(self, x):
         """[K, ...] outputs of every teacher on ``x`` (batched path)."""
@@ -175,17 +191,21 @@ class TeacherEnsemble(object):
                 self._fall_back(f"the replay raised {type(e).__name__} on a later batch: {e}")
                 return self._vmap_logits(x)
         # first use: the program must reproduce the vmap'd forward (same
-        # graph, f32 matrix-core arithmetic: normwise), else it is dropped
-        ref = self._vmap_logits(x)
+        # graph, f32 matrix-core arithmetic: normwise) on the checked
+        # teachers, else it is dropped
+        rows = self._check_rows()
+        ref = self._vmap_logits(x, rows)
         try:
             got = self.program(x)
+            cmp = got if rows is None else got[rows]
             why = None
-            if got.shape != ref.shape:
-                why = f"its output shape {tuple(got.shape)} is not {tuple(ref.shape)}"
-            elif not bool((torch.isfinite(got) == torch.isfinite(ref)).all()):
+            if got.shape[0] != self.K or cmp.shape != ref.shape:
+                why = (f"its output shape {tuple(got.shape)} is not "
+                       f"{(self.K,) + tuple(ref.shape[1:])}")
+            elif not bool((torch.isfinite(cmp) == torch.isfinite(ref)).all()):
                 why = "its first batch has non-finite values where the vmap'd forward has not"
             else:
-                err = float(torch.linalg.vector_norm((got - ref).double().nan_to_num()))
+                err = float(torch.linalg.vector_norm((cmp - ref).double().nan_to_num()))
                 ref_n = float(torch.linalg.vector_norm(ref.double().nan_to_num()))
                 if err > 1e-4 * ref_n + 1e-30:
                     why = (f"its first batch differs from the vmap'd forward (normwise "
@@ -196,7 +216,7 @@ class TeacherEnsemble(object):
         if why is not None:
             self.program = None
             self._fall_back(why)
-            return ref
+            return ref if rows is None else self._vmap_logits(x)
         return got
 
     def _sequential_mean(self, x):

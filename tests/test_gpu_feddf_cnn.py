@@ -185,9 +185,12 @@ def test_replay_fallback_is_counted_and_warned():
     assert ens.stats()["fallbacks"] == 1 and not ens.stats()["replayed"]
 
 
-def test_replay_first_batch_mismatch_is_counted():
+@pytest.mark.parametrize("K", [4, 100])
+def test_replay_first_batch_mismatch_is_counted(K):
     """A replay whose first batch disagrees with the vmap'd forward is
-    dropped, counted and reported with its error."""
+    dropped, counted and reported with its error; above 64 teachers the check
+    compares the first and last 32 and the fallback still returns every
+    teacher's vmap'd logits."""
     from fedsim_amd.distributed.centralized.training.feddf import TeacherEnsemble
     from fedsim_amd.utils import vectorize_module
 
@@ -195,16 +198,41 @@ def test_replay_first_batch_mismatch_is_counted():
     torch.manual_seed(12)
     model = S.TinyModel().to(dev)
     base = vectorize_module(model)
-    ens = TeacherEnsemble(model, [base + 0.05 * torch.randn_like(base) for _ in range(4)], dev)
+    teachers = [base + 0.05 * torch.randn_like(base) for _ in range(K)]
+    ens = TeacherEnsemble(model, teachers, dev)
     assert ens.program is not None
+    rows = ens._check_rows()
+    assert (rows is None) == (K <= 64) and (rows is None or rows.numel() == 64)
     real = ens.program.__call__
     ens.program.__class__ = type("Broken", (ens.program.__class__,),
                                  {"__call__": lambda self, x: real(x) * 1.01})
+    x = torch.randn(8, 37, device=dev)
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        ens.mean_logits(torch.randn(8, 37, device=dev))
+        got = ens.mean_logits(x)
     assert ens.program is None and ens.fallbacks == 1
     assert "first batch differs" in ens.fallback_reason
+    per = torch.stack([ens._forward(t, x) for t in teachers])
+    torch.testing.assert_close(got, per.mean(0), rtol=1e-5, atol=1e-6)
+
+
+def test_replay_kept_on_many_teachers():
+    """Above 64 teachers the sampled check keeps a correct replay, and its
+    logits are every teacher's forward."""
+    from fedsim_amd.distributed.centralized.training.feddf import TeacherEnsemble
+    from fedsim_amd.utils import vectorize_module
+
+    dev = torch.device("cuda")
+    torch.manual_seed(13)
+    model = S.TinyModel().to(dev)
+    base = vectorize_module(model)
+    teachers = [base + 0.05 * torch.randn_like(base) for _ in range(130)]
+    ens = TeacherEnsemble(model, teachers, dev)
+    x = torch.randn(8, 37, device=dev)
+    logits = ens.teacher_logits(x)
+    assert ens.program is not None and ens.fallbacks == 0 and logits.shape[0] == 130
+    per = torch.stack([ens._forward(t, x) for t in teachers])
+    torch.testing.assert_close(logits, per, rtol=1e-5, atol=1e-6)
 
 
 class _Jitter(torch.utils.data.Dataset):
