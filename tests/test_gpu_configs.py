@@ -304,7 +304,7 @@ def _gpu_slab_client(record, cols, slab_row=True):
 
 
 @pytest.mark.parametrize("slab_row", [True, False], ids=["slab_rows", "borrowed"])
-@pytest.mark.parametrize("algo", ["FedAvg", "AdaBest"])
+@pytest.mark.parametrize("algo", ["FedAvg", "AdaBest", "FedNova"])
 def test_configs_2_3_full_participation_1000x1_085_668(algo, slab_row):
     """(e) -c 1.0: K = 1000 clients x SimpleCNN2's 1 085 668 parameters, one
     round through the round driver with every client in a slab row, or
@@ -349,9 +349,12 @@ def test_configs_2_3_full_participation_1000x1_085_668(algo, slab_row):
     assert split and all(split)  # the split pop + step at this size
     assert borrowed == [not slab_row]  # rows read in the slab, or where the clients left them
     sub = torch.stack([v for v, _ in record]).cpu().numpy()  # [K, n] in arrival order
-    w = [n for _, n in record] if algo == "FedAvg" else [1] * n_clients
+    # FedAvg: n_train (int); AdaBest: 1; FedNova: n_train / num_steps (float,
+    # fednova.py:58-59; the client sends num_steps = max(1, n // 32))
+    w = {"FedAvg": [n for _, n in record], "AdaBest": [1] * n_clients,
+         "FedNova": [n / max(1, n // 32) for _, n in record]}[algo]
     avg = ref.reduce(sub, w, W=sum(w))
-    if algo == "FedAvg":
+    if algo in ("FedAvg", "FedNova"):
         state = ref.ServerState("fedavg", cloud0, dict(lr=1.0))
     else:
         state = ref.ServerState("adabest", cloud0, dict(lr=1.0), aux=prev0, coef=0.6)
