@@ -32,6 +32,7 @@ torch.distributed.run; either way rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib
 import json
 import os
@@ -334,19 +335,42 @@ def make_pool(rk, R, P, C, seed):
     return Xb
 
 
-def load_pmc(path, K, P, kernel, layout, step):
+def _md5(path):
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def load_pmc(path, K, P, kernel, layout, step, lib_path):
     """HBM bytes per launch from the committed PMC summary
-    (tools/pmc_traffic.py), when it was measured on this exact kernel and
-    workload; else None."""
+    (tools/pmc_traffic.py), with where it came from.  The bytes are reported
+    only when the summary was measured on this exact kernel and workload AND
+    on this build of libfedagg.so (md5 of the library this process loaded);
+    otherwise traffic is None and the source says why.  Returns (traffic,
+    source)."""
     try:
         with open(path) as f:
             d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if d.get("K") == K and d.get("P") == P and d.get("kernel") == kernel and \
-            d.get("layout", "strided") == layout and d.get("step", "split") == step:
-        return d.get("hbm_bytes_per_launch")
-    return None
+    except (OSError, ValueError) as e:
+        return None, dict(summary=os.path.relpath(path, REPO), reason=f"unreadable: {e}")
+    src = dict(d.get("source") or {})
+    src["summary"] = os.path.relpath(path, REPO)
+    try:
+        here = _md5(lib_path)
+    except OSError:
+        here = None
+    src["lib_md5_loaded"] = here
+    if not (d.get("K") == K and d.get("P") == P and d.get("kernel") == kernel and
+            d.get("layout", "strided") == layout and d.get("step", "split") == step):
+        src["reason"] = "the summary was measured on another kernel / workload"
+        return None, src
+    if src.get("lib_md5") is None or src.get("lib_md5") != here:
+        src["reason"] = "the summary was measured on another build of libfedagg.so"
+        return None, src
+    src["reason"] = "same kernel, workload and build (PMC FETCH_SIZE + WRITE_SIZE passes)"
+    return d.get("hbm_bytes_per_launch"), src
 
 
 def _cpu_model():
@@ -486,9 +510,11 @@ def setup_param(a, rk, clock):
     info["_kernel"] = "%s (%s)" % (kernel,
         "fedagg_reduce_step_blocked_f32, EpiStep<FEDAVG>" if fused else
         "fedagg_reduce_blocked_f32" if a.layout == "blocked" else "fedagg_reduce_f32")
+    from fedsim_amd import _native
+
     info["_traffic"] = load_pmc(a.pmc_json, K, P, kernel,
                                 a.layout if a.layout == "strided" else f"blocked{a.C}",
-                                step_mode)
+                                step_mode, _native.LIB_PATH)
     return step, info, 4.0 * K * P * rk.world, (X, avg, cloud, grad)
 
 
@@ -599,7 +625,7 @@ def setup_streamed(a, rk, clock):
               else "reordered across ranks (normwise <= 1e-6 vs reference CPU)"),
         layout=f"blocked C={C}", step="fused" if fuse_last else "split")
     info["_kernel"] = kname
-    info["_traffic"] = None
+    info["_traffic"] = (None, dict(reason="no PMC summary is kept for the streamed modes"))
     total = 4.0 * K * (a.P if a.mode == "strong" else P * rk.world)
     return step, info, total, (pool, acc, cloud, grad), ar_ms
 
@@ -649,7 +675,7 @@ def _main(a, quiet):
 
     value = total_bytes * a.steps / elapsed / 1e9
     kernel = info.pop("_kernel", None)
-    traffic = info.pop("_traffic", None)
+    traffic, traffic_source = info.pop("_traffic", (None, None))
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -686,6 +712,7 @@ def _main(a, quiet):
             "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBPS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "launch_ms": round(kern_ms_max, 4),
             "alg_bytes_per_launch": nbytes,
         }

@@ -50,6 +50,66 @@ def _from_host(obj, device):
     return obj
 
 
+_SKIP = object()
+
+
+def _plain(v):
+    """A picklable, exactly comparable image of a plain-data value (floats by
+    their hex form, small tensors by value); _SKIP for anything else (models,
+    large tensors, objects)."""
+    if v is None or isinstance(v, (bool, int, str)):
+        return v
+    if isinstance(v, float):
+        return ("f", v.hex())
+    if type(v).__module__ == "numpy" and hasattr(v, "item") and getattr(v, "ndim", 1) == 0:
+        return _plain(v.item())
+    if isinstance(v, (list, tuple)):
+        items = tuple(_plain(x) for x in v)
+        return _SKIP if any(x is _SKIP for x in items) else (type(v).__name__, items)
+    if isinstance(v, torch.Tensor) and v.numel() <= 16 and v.device.type != "meta":
+        vals = v.detach().cpu().reshape(-1).double().tolist()
+        return ("t", str(v.dtype), tuple(v.shape), tuple(float(x).hex() for x in vals))
+    return _SKIP
+
+
+def _context_fingerprint(ctx) -> Optional[dict]:
+    """The plain-data entries of a send_to_client message (e.g. AdaBest's
+    ``average_sample``): what a client-sharded round compares to find clients
+    whose context depends on earlier clients' receive_from_client."""
+    if not isinstance(ctx, dict):
+        return None
+    out = {}
+    for k, v in ctx.items():
+        fp = _plain(v)
+        if fp is not _SKIP:
+            out[k] = fp
+    return out
+
+
+def _storage_state(st: Storage):
+    """What a client storage holds now: its entries by reference, plus the
+    version counter of each tensor (an in-place change shows there)."""
+    items = dict(st._storage)
+    versions = {k: obj._version for k, (obj, _, _) in items.items()
+                if isinstance(obj, torch.Tensor)}
+    return items, versions
+
+
+def _changed_keys(st: Storage, state) -> list:
+    items, versions = state
+    out = []
+    for k, entry in st._storage.items():
+        old = items.get(k)
+        obj = entry[0]
+        if old is None or old[0] is not obj or entry[1:] != old[1:]:
+            out.append(k)
+        elif isinstance(obj, torch.Tensor) and obj._version != versions.get(k):
+            out.append(k)
+        elif not isinstance(obj, (torch.Tensor, type(None), bool, int, float, str, tuple)):
+            out.append(k)  # a mutable object: it may have changed in place
+    return out
+
+
 def _distributed_rank() -> int:
     d = torch.distributed
     return d.get_rank() if d.is_available() and d.is_initialized() else 0
@@ -79,6 +139,7 @@ class CentralFLAlgorithm(object):
         shard_over=None,
         shard_clients=None,
         client_reduction="chain",
+        check_client_context=True,
         progress=False,
         **kwargs,
     ):
@@ -162,6 +223,12 @@ class CentralFLAlgorithm(object):
         elif shard_over is not None:
             raise ValueError("pass either aggregator_factory or shard_over")
         self._aggregator_factory = aggregator_factory
+        # client-sharded rounds: check that no client's send_to_client
+        # message depends on an earlier client of the same round
+        self._check_client_context = check_client_context
+        # client-storage entries another rank wrote, kept in host memory
+        # until this rank trains that client: {client_id: {key: device kind}}
+        self._client_on_host = {}
         self._progress = progress
         self._server_memory = Storage()
         w = self._server_memory.write
@@ -226,7 +293,7 @@ class CentralFLAlgorithm(object):
     def _send_to_client(self, client_id):
         return self.user_methods["send_to_client"](self._server_memory, client_id=client_id)
 
-    def _send_to_server(self, client_id):
+    def _send_to_server(self, client_id, ctx_hook=None):
         r2r = self._server_memory.read("r2r_local_lr_scheduler")
         data_manager = self._server_memory.read("data_manager", silent=True)
         rounds = self._server_memory.read("rounds")
@@ -234,13 +301,16 @@ class CentralFLAlgorithm(object):
         local_optimizer_def = cfg.read("local_optimizer_def")
         if r2r is not None:
             local_optimizer_def = partial(local_optimizer_def, lr=r2r.get_last_lr()[0])
+        ctx = self._send_to_client(client_id)
+        if ctx_hook is not None:
+            ctx_hook(ctx)
         client_ctx = self.user_methods["send_to_server"](
             client_id, rounds, self._client_memory[client_id],
             data_manager.get_local_dataset(client_id), self.get_train_split_name(),
             self.get_local_scores(), cfg.read("epochs"), cfg.read("criterion_def")(),
             cfg.read("batch_size"), cfg.read("test_batch_size"), local_optimizer_def,
             cfg.read("local_lr_scheduler_def"), cfg.read("device"),
-            ctx=self._send_to_client(client_id),
+            ctx=ctx,
         )
         if not isinstance(client_ctx, dict):
             raise Exception("client should only return a dict!")
@@ -312,65 +382,134 @@ class CentralFLAlgorithm(object):
         the round's messages in the reference's order (other ranks' vectors as
         RemoteRow stand-ins), so the server state evolves identically on every
         rank.  Clients' own storages (AdaBest / FedDyn drift state) are
-        shared with every rank after the round.  Returns ``diverged``."""
-        from ...sharding import RemoteRow
+        shared with every rank after the round.  Returns ``diverged``.
 
+        Checked on every rank alike (so all raise together, none hangs):
+        * every rank sampled the same clients (a client that consumes Python
+          ``random`` on one rank would otherwise shift the next rounds);
+        * (``check_client_context``) every client's send_to_client message
+          is the one it would get in the reference's sequential loop: at
+          position p the message is recomputed after the receives of clients
+          0..p-1 and its plain-data entries must equal what the client
+          trained with.  AdaBest's ``average_sample`` (the running mean that
+          receive_from_client updates, adabest.py:76-80,167-169) differs, so
+          such an algorithm is refused instead of run on stale contexts."""
         clients = self._sample_clients()  # same seed, same list on every rank
         lo, hi = agg.client_block(len(clients))
-        local, failure = {}, None
+        local, failure, ctx_fp, before = {}, None, {}, {}
         try:
             for p in range(lo, hi):
-                local[p] = self._send_to_server(clients[p])
+                cid = clients[p]
+                self._client_to_device(cid, agg)
+                before[p] = _storage_state(self._client_memory[cid])
+                local[p] = self._send_to_server(
+                    cid, ctx_hook=lambda ctx, p=p: ctx_fp.__setitem__(p, _context_fingerprint(ctx)))
         except Exception as e:  # noqa: BLE001 - re-raised below, after the exchange
             failure, local = e, {}
         # every rank reaches the exchange, so a failing client cannot leave
         # the others blocked in it; then every rank raises
-        remote = agg.exchange(local, len(clients), failed=failure is not None)
+        remote, extras = agg.exchange(local, len(clients), failed=failure is not None,
+                                      extras=dict(clients=list(clients), ctx=ctx_fp))
         if failure is not None:
             raise failure
         if remote is None:
             raise RuntimeError("a client of another rank of this client-sharded round failed")
-        diverged = False
+        if any(e["clients"] != list(clients) for e in extras):
+            raise RuntimeError(
+                "the ranks of a client-sharded round sampled different clients (%s): every "
+                "rank must draw the same Python random numbers between rounds (a client "
+                "that consumes Python's random module desynchronises them)"
+                % "; ".join("rank %d: %s" % (r, e["clients"][:8]) for r, e in enumerate(extras)))
+        contexts = {}
+        for e in extras:
+            contexts.update(e["ctx"])
+        diverged_at = None
         for p in range(len(clients)):
+            if p > 0 and self._check_client_context:
+                now = _context_fingerprint(self._send_to_client(clients[p]))
+                if now != contexts.get(p):
+                    keys = sorted(k for k in set(now or {}) | set(contexts.get(p) or {})
+                                  if (now or {}).get(k) != (contexts.get(p) or {}).get(k))
+                    raise RuntimeError(
+                        f"client-sharded round: client {clients[p]} (position {p}) trained with "
+                        f"a send_to_client message whose {keys} differ from the one the "
+                        "reference's sequential loop gives it after the earlier clients' "
+                        "receive_from_client; this algorithm's clients depend on each other in "
+                        "arrival order (e.g. AdaBest's running average_sample) and cannot be "
+                        "trained in parallel -- use shard_over (parameter sharding) instead")
             client_msg = local.pop(p) if p in local else remote[p]
             remote[p] = None
             success = self._receive_from_client(client_msg, agg, appendix_aggregator)
             del client_msg
             if not success:
-                diverged = True
+                diverged_at = p
                 break
         local.clear()
-        self._share_client_memory(agg, clients[lo:hi])
-        for key in appendix_aggregator.keys():
-            if any(isinstance(v, RemoteRow) for v in appendix_aggregator.get_values(key)):
-                raise NotImplementedError(
-                    "client-sharded rounds keep each client vector on the rank that trained it; "
-                    f"{key!r} keeps every client's vector (FedDF): use shard_over instead")
-        return diverged
+        # the reference stops training at the diverged client: clients after
+        # it keep the storage they had before this round
+        shared = []
+        for p in range(lo, hi):
+            if diverged_at is not None and p > diverged_at:
+                self._restore_client(clients[p], before[p])
+            else:
+                shared.append((clients[p], before[p]))
+        self._share_client_memory(agg, shared)
+        return diverged_at is not None
+
+    def _restore_client(self, cid, state) -> None:
+        items, versions = state
+        st = self._client_memory[cid]
+        for k, (obj, _, _) in items.items():
+            if isinstance(obj, torch.Tensor) and obj._version != versions.get(k):
+                import warnings
+
+                warnings.warn(f"client {cid}'s storage entry {k!r} was changed in place by a "
+                              "client after the diverged one; it cannot be restored",
+                              RuntimeWarning, stacklevel=3)
+        st._storage = dict(items)
+
+    def _client_to_device(self, cid, agg) -> None:
+        """Entries other ranks wrote for this client wait in host memory
+        until this rank trains it."""
+        pending = self._client_on_host.pop(cid, None)
+        if not pending:
+            return
+        dev = agg._reduce_device()
+        st = self._client_memory[cid]
+        for k, (kind, rg) in pending.items():
+            obj, rp, wp = st._storage[k]
+            st._storage[k] = (_from_host(("__fedsim_tensor__", obj, kind, rg), dev), rp, wp)
 
     def _share_client_memory(self, agg, trained) -> None:
-        """Every rank gets the client storages this round's other ranks wrote
-        (tensors travel through host memory and land on this rank's device)."""
+        """Every rank gets the client-storage entries this round's other
+        ranks wrote (only the entries that changed; tensors travel through
+        host memory and stay there until this rank trains that client)."""
         import torch.distributed as dist
-
-        def portable(st):
-            return [(k, _to_host(obj), rp, wp) for k, (obj, rp, wp) in st._storage.items()]
 
         if agg._solo:
             return
-        mine = {cid: portable(self._client_memory[cid]) for cid in trained
-                if len(self._client_memory[cid].get_all_keys())}
+        mine = {}
+        for cid, state in trained:
+            st = self._client_memory[cid]
+            keys = _changed_keys(st, state)
+            if keys:
+                mine[cid] = [(k, _to_host(st._storage[k][0]), st._storage[k][1],
+                              st._storage[k][2]) for k in keys]
         every = [None] * agg.world_size
         dist.all_gather_object(every, mine, group=agg._group)
-        dev = agg._reduce_device()
         for r, mem in enumerate(every):
             if r == agg.rank:
                 continue
             for cid, items in mem.items():
-                st = Storage()
+                st = self._client_memory[cid]
+                pending = self._client_on_host.setdefault(cid, {})
                 for k, obj, rp, wp in items:
-                    st._storage[k] = (_from_host(obj, dev), rp, wp)
-                self._client_memory[cid] = st
+                    pending.pop(k, None)
+                    if isinstance(obj, tuple) and len(obj) == 4 and obj[0] == "__fedsim_tensor__":
+                        _, t, kind, rg = obj
+                        pending[k] = (kind, rg)
+                        obj = t.requires_grad_(rg) if rg else t
+                    st._storage[k] = (obj, rp, wp)
 
     def _at_round_start(self) -> None:
         self.user_methods["at_round_start"](self._server_memory)

@@ -225,15 +225,32 @@ class TeacherEnsemble(object):
             agg.add("target", self._forward(self.slab[k], x).clone(), 1)
         return agg.get("target")
 
+    def _batched_logits(self, x):
+        """[K, ...] teacher outputs on the batched path, or None when it
+        raised (counted; the per-teacher path takes over)."""
+        try:
+            return self.teacher_logits(x)
+        except Exception as e:  # noqa: BLE001 - e.g. random ops under vmap
+            self.batched, self.program = False, None
+            self._fall_back(f"the vmap'd forward raised {type(e).__name__}: {e}")
+            return None
+
+    @torch.no_grad()
+    def logit_rows(self, x):
+        """Every teacher's output on ``x`` as the rows of a [K, n] fp32 slab,
+        and the output shape: what a client-sharded round sums across ranks."""
+        logits = self._batched_logits(x) if self.batched else None
+        if logits is None:
+            logits = torch.stack([self._forward(self.slab[k], x).clone() for k in range(self.K)])
+        K, shape = logits.shape[0], logits.shape[1:]
+        return logits.reshape(K, -1).float().contiguous(), shape
+
     @torch.no_grad()
     def mean_logits(self, x):
         if not self.batched:
             return self._sequential_mean(x)
-        try:
-            logits = self.teacher_logits(x)
-        except Exception as e:  # noqa: BLE001 - e.g. random ops under vmap
-            self.batched, self.program = False, None
-            self._fall_back(f"the vmap'd forward raised {type(e).__name__}: {e}")
+        logits = self._batched_logits(x)
+        if logits is None:
             return self._sequential_mean(x)
         K, shape = logits.shape[0], logits.shape[1:]
         rows = logits.reshape(K, -1).float().contiguous()
@@ -247,6 +264,78 @@ class TeacherEnsemble(object):
         """Leave the model holding the last teacher, as the reference's
         per-teacher initialize_module does (feddf.py:119)."""
         initialize_module(self.model, self.slab[-1])
+
+
+class ShardedTeachers(object):
+    """FedDF's teachers in a client-sharded round
+    (``CentralFLAlgorithm(..., shard_clients=...)``): each rank holds the
+    vectors of the clients it trained (the others are RemoteRow stand-ins in
+    the appendix aggregator), replays its own teachers -- the same
+    TeacherEnsemble kernels, K/N teachers per GPU -- and the per-rank logit
+    sums are combined by the round's ClientShardedSerialAggregator:
+    ``chain`` adds rank after rank in arrival order, the reference's
+    ``target_agg.add(target, 1)`` x K order bit for bit (feddf.py:120-126);
+    ``allreduce`` sums from +0 per rank and all-reduces (normwise).  Then
+    the divide by fl32(K) (``get``, feddf.py:126) and the same student step
+    on every rank."""
+
+    def __init__(self, model, values, agg, device):
+        from ....sharding import RemoteRow
+
+        me = agg.rank
+        self.agg = agg
+        self.model = model
+        self.K = len(values)
+        seq = [v.owner if isinstance(v, RemoteRow) else me for v in values]
+        self.owners = [r for i, r in enumerate(seq) if i == 0 or seq[i - 1] != r]
+        self.last_owner = seq[-1]
+        local = [v for v in values if not isinstance(v, RemoteRow)]
+        self.local = TeacherEnsemble(model, local, device) if local else None
+
+    @property
+    def deterministic(self) -> bool:
+        # agreed by every rank: a batch's targets are reused on all or none
+        return self.agg._all_true(self.local is None or self.local.deterministic)
+
+    def stats(self) -> dict:
+        st = self.local.stats() if self.local is not None else dict(
+            replayed=False, batched=False, fallbacks=0, reason=None, linear_launches=0,
+            conv_launches=0, pool_launches=0, fused_pools=0)
+        return dict(st, teachers_total=self.K,
+                    teachers_local=0 if self.local is None else self.local.K,
+                    rank=self.agg.rank, client_reduction=self.agg.mode)
+
+    @torch.no_grad()
+    def mean_logits(self, x):
+        if self.local is not None:
+            rows, shape = self.local.logit_rows(x)
+        else:  # no teacher on this rank: only the output's shape is needed
+            rows, shape = None, self.model(x).shape
+        n = 1
+        for d in shape:
+            n *= d
+        s = self.agg.ordered_rows_sum(rows, self.owners, n)
+        return self.agg.divide(s, self.K).view(shape).to(x.device)
+
+    def load_last(self):
+        """The model holds the last teacher afterwards, as after the
+        reference's loop (feddf.py:122): broadcast from the rank holding it."""
+        dev = self.agg._reduce_device()
+        P = sum(p.numel() for p in self.model.parameters())
+        if self.agg.rank == self.last_owner:
+            vec = self.local.slab[-1].to(dev).contiguous().clone()
+        else:
+            vec = torch.empty(P, dtype=torch.float32, device=dev)
+        self.agg.broadcast_from(vec, self.last_owner)
+        initialize_module(self.model, vec.to(next(self.model.parameters()).device))
+
+
+def _teachers(model, values, serial_aggregator, device):
+    """The round's teacher ensemble: split over the ranks of a
+    client-sharded round (decided alike on every rank), else one slab."""
+    if getattr(serial_aggregator, "collective", False):
+        return ShardedTeachers(model, values, serial_aggregator, device)
+    return TeacherEnsemble(model, values, device)
 
 
 class FedDF(FedAvg):
@@ -281,8 +370,8 @@ class FedDF(FedAvg):
             lr_scheduler = server_storage.read("lr_scheduler")
             device = server_storage.read("device")
 
-            teachers = TeacherEnsemble(model, appendix_aggregator.get_values("local_params"),
-                                       device)
+            teachers = _teachers(model, appendix_aggregator.get_values("local_params"),
+                                 serial_aggregator, device)
             # the same batches every epoch: mean logits computed once, reused
             # for a batch whose input is the same value again
             cache = [] if (global_epochs > 1 and _in_order(train_data_loader)

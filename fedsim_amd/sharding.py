@@ -626,30 +626,10 @@ class _ClientShardEntry(_TensorEntry):
         it for the same key, as SPMD ``optimize`` does)."""
         if self.sum is not None:
             return self.sum
-        agg = self.agg
-        me = agg.rank
-        if agg._solo:
-            buf = self.local.partial(None)
-        elif agg.mode == "allreduce":
-            buf = (self.local.partial(None) if self.local is not None
-                   else torch.zeros(self.P, dtype=torch.float32, device=self.dev))
-            _all_reduce_sum(buf, agg._group)
-        else:
-            if len(set(self.owners)) != len(self.owners):
-                raise RuntimeError("client_reduction='chain' needs each rank's clients to be one "
-                                   "contiguous run of the round's arrival order")
-            if me in self.owners:
-                i = self.owners.index(me)
-                acc_in = None
-                if i > 0:
-                    acc_in = torch.empty(self.P, dtype=torch.float32, device=self.dev)
-                    _recv(acc_in, _global_rank(agg._group, self.owners[i - 1]), agg._group)
-                buf = self.local.partial(acc_in)
-                if i + 1 < len(self.owners):
-                    _send(buf, _global_rank(agg._group, self.owners[i + 1]), agg._group)
-            else:
-                buf = torch.empty(self.P, dtype=torch.float32, device=self.dev)
-            _broadcast(buf, _global_rank(agg._group, self.owners[-1]), agg._group)
+        local = self.local
+        chainable = local is None or getattr(local, "chainable", lambda: True)()
+        buf = self.agg._ordered_sum(self.owners, None if local is None else local.partial,
+                                    self.P, chainable)
         self.local = None
         self.sum = buf
         return buf
@@ -658,9 +638,7 @@ class _ClientShardEntry(_TensorEntry):
         s = self._global_sum()
         if not self._weighted():
             return s.clone()
-        if s.device.type == "cuda":
-            return ops.finalize(s, self.cur_w)
-        return s / ops.fl32(self.cur_w)  # CPU gloo rehearsal: ATen's true divide
+        return self.agg.divide(s, self.cur_w)
 
     def _deliver(self, t: torch.Tensor) -> torch.Tensor:
         t = t.view(self.shape)
@@ -742,6 +720,11 @@ class ClientShardedSerialAggregator(SerialAggregator):
     def world_size(self) -> int:
         return self._world
 
+    @property
+    def collective(self) -> bool:
+        """Whether this round spans several ranks (collectives run)."""
+        return not self._solo
+
     def client_block(self, n: int):
         """[lo, hi): the positions of the round's n sampled clients this rank
         trains (one contiguous block each, in rank order)."""
@@ -758,7 +741,104 @@ class ClientShardedSerialAggregator(SerialAggregator):
         if self._entry_factory is not None:
             return self._entry_factory(value, self)
         dev = self._reduce_device()
-        return _DeviceEntry(value, dev, self._opts, self, out_device=dev)
+        e = _DeviceEntry(value, dev, self._opts, self, out_device=dev)
+        if self.mode == "chain":
+            # a chained partial continues the previous rank's sum, so no row
+            # may be drained from +0 before it: hold every borrowed row (the
+            # round's local messages are all alive until received anyway)
+            e.Bmax = 1 << 62
+        return e
+
+    # -- collectives shared by the tensor keys and FedDF's teacher targets --
+    def _all_true(self, flag: bool) -> bool:
+        """Collective AND of a per-rank flag (one int32 all-reduce MIN), so
+        every rank takes the same branch -- or raises -- together."""
+        if self._solo:
+            return bool(flag)
+        dev = self._reduce_device()
+        if dist.get_backend(self._group) == dist.Backend.GLOO:
+            dev = torch.device("cpu")
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._group)
+        return bool(t.item())
+
+    def _ordered_sum(self, owners: Sequence[int], local_partial: Optional[Callable], P: int,
+                     chainable: bool = True) -> torch.Tensor:
+        """Collective: the sum over every rank's rows.  ``owners`` are the
+        ranks holding rows, in arrival order (one contiguous run each);
+        ``local_partial(acc_in)`` (None when this rank holds no rows) reduces
+        this rank's rows in order onto ``acc_in`` (None: from +0).
+        chain: rank after rank in ``owners`` order, then a broadcast of the
+        last owner's sum (bit-exact arrival order); allreduce: partial sums
+        from +0 and one all-reduce(sum) (reordered)."""
+        me = self.rank
+        if self._solo:
+            return local_partial(None)
+        if self.mode == "allreduce":
+            buf = (local_partial(None) if local_partial is not None
+                   else torch.zeros(P, dtype=torch.float32, device=self._reduce_device()))
+            _all_reduce_sum(buf, self._group)
+            return buf
+        if len(set(owners)) != len(owners):
+            raise RuntimeError("client_reduction='chain' needs each rank's clients to be one "
+                               "contiguous run of the round's arrival order")
+        # decided together: a rank that cannot continue the chain (rows
+        # already drained from +0) must not leave the others blocked in recv
+        if not self._all_true(chainable):
+            raise RuntimeError(
+                "client_reduction='chain': a rank drained rows of this key from +0 before "
+                "the chain reached it (ring full, or host and HBM rows mixed), so the "
+                "arrival-order sum cannot be continued bit for bit; raise slab_bytes / "
+                "max_rows, or use client_reduction='allreduce'")
+        if me in owners:
+            i = owners.index(me)
+            acc_in = None
+            if i > 0:
+                acc_in = torch.empty(P, dtype=torch.float32, device=self._reduce_device())
+                _recv(acc_in, _global_rank(self._group, owners[i - 1]), self._group)
+            buf = local_partial(acc_in)
+            if i + 1 < len(owners):
+                _send(buf, _global_rank(self._group, owners[i + 1]), self._group)
+        else:
+            buf = torch.empty(P, dtype=torch.float32, device=self._reduce_device())
+        _broadcast(buf, _global_rank(self._group, owners[-1]), self._group)
+        return buf
+
+    def divide(self, s: torch.Tensor, W) -> torch.Tensor:
+        """fl32(s / fl32(W)), the reference's ``get`` divide."""
+        if s.device.type == "cuda":
+            return ops.finalize(s, W)
+        return s / ops.fl32(W)  # CPU gloo rehearsal: ATen's true divide
+
+    def ordered_rows_sum(self, rows: Optional[torch.Tensor], owners: Sequence[int],
+                         n: int) -> torch.Tensor:
+        """Collective: the weight-1 sum of every rank's rows ([K_r, n] on rank
+        r, None when it holds none), in arrival order under ``chain`` -- the
+        reference's ``add(x, 1)`` x K order (FedDF's teacher targets,
+        feddf.py:120-126) -- or reordered under ``allreduce``."""
+        dev = self._reduce_device()
+        local_partial = None
+        if rows is not None and rows.shape[0] > 0:
+            if self._entry_factory is not None:
+                def local_partial(acc_in):
+                    e = self._entry_factory(rows[0], self)
+                    for r in rows:
+                        e.add(r, 1)
+                    return e.partial(acc_in)
+            else:
+                def local_partial(acc_in):
+                    X = rows if rows.device == dev else rows.to(dev)
+                    X = X.reshape(X.shape[0], -1).contiguous()
+                    out = torch.empty(n, dtype=torch.float32, device=dev)
+                    ones = torch.ones(X.shape[0], dtype=torch.float32, device=dev)
+                    return ops.reduce_slab(X, ones, out, acc_in=acc_in)
+        return self._ordered_sum(owners, local_partial, n)
+
+    def broadcast_from(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        """Collective: ``t`` on rank ``src`` copied into ``t`` on every rank."""
+        if not self._solo:
+            _broadcast(t, _global_rank(self._group, src), self._group)
+        return t
 
     def _apply_step(self, step: ops.ServerStep, avg: torch.Tensor) -> None:
         if self._step_impl is not None:
@@ -782,27 +862,31 @@ class ClientShardedSerialAggregator(SerialAggregator):
             return
         super().add(key, value, weight)
 
-    def exchange(self, local_msgs: dict, n: int, failed: bool = False) -> Optional[list]:
+    def exchange(self, local_msgs: dict, n: int, failed: bool = False, extras=None):
         """Every rank's client messages of this round, position by position:
         this rank's own as given, the others' rebuilt from what their ranks
         sent (tensors as RemoteRow stand-ins, 0-dim tensors and everything
         else by value).  Collective.  ``failed``: this rank's clients raised;
-        every rank then gets None (and raises), none is left waiting."""
+        every rank then gets None (and raises), none is left waiting.
+        ``extras``: any picklable per-rank value; with it, returns
+        ``(messages, [extras of rank 0, 1, ...])``."""
         if self._solo:
-            return None if failed else [None] * n
+            msgs = None if failed else [None] * n
+            return msgs if extras is None else (msgs, [extras])
         mine = None if failed else {p: _skeleton(m, self._rank) for p, m in local_msgs.items()}
         every = [None] * self._world
-        dist.all_gather_object(every, mine, group=self._group)
-        if any(m is None for m in every):
-            return None
+        dist.all_gather_object(every, (mine, extras), group=self._group)
+        got = [e[1] for e in every]
+        if any(e[0] is None for e in every):
+            return None if extras is None else (None, got)
         dev = self._reduce_device()
         out = [None] * n
-        for r, msgs in enumerate(every):
+        for r, (msgs, _) in enumerate(every):
             if r == self._rank:
                 continue
             for p, m in msgs.items():
                 out[p] = _flesh(m, dev)
-        return out
+        return out if extras is None else (out, got)
 
     def reserve(self, key, P, device):
         """No reserved rows: a rank trains all its clients before any of them

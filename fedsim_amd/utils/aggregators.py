@@ -438,6 +438,11 @@ class _DeviceEntry(_TensorEntry):
         self.acc = None
         return out
 
+    def chainable(self) -> bool:
+        """Whether ``partial`` can still continue another rank's sum: no row
+        has been drained into the accumulator from +0 yet."""
+        return self.acc is None
+
     def partial(self, acc_in: Optional[torch.Tensor], W=None) -> torch.Tensor:
         """This key's rows reduced in arrival order ONTO ``acc_in`` (None:
         from +0), divided by fl32(W) when W is given; releases the rows.  The

@@ -131,5 +131,22 @@ def cloud_vector(P: int, seed: int) -> np.ndarray:
     )
 
 
+def teacher_vectors(init: np.ndarray, K: int, seed: int, n_base: int = 16, scale: float = 0.02):
+    """K FedDF teacher vectors around a model's init cloud, generated one at a
+    time (nothing K x P is ever held): teacher k = fl32(init + fl32(c_k *
+    roll(D_{k mod n_base}, 7919 k mod P))), with n_base shared deltas
+    D_j = fl32(scale * N(0, 1)) and c_k in [0.5, 1.5).  Only fp32 elementwise
+    multiplies and adds (one rounding each) and a permutation, so every
+    platform regenerates the same bits; 16 hashed deltas keep 1000 teachers at
+    a few seconds instead of a hash per teacher."""
+    init = np.ascontiguousarray(init, dtype=np.float32)
+    P = init.size
+    D = [(scale * gauss(seed * 7919 + 31 + j, P)).astype(np.float32) for j in range(n_base)]
+    c = (0.5 + uniform01(seed * 13 + 5, K)).astype(np.float32)
+    for k in range(K):
+        d = np.roll(D[k % n_base], (k * 7919) % P)
+        yield init + c[k] * d
+
+
 def sha256(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()

@@ -68,8 +68,19 @@ class ChainOracleEntry(OracleEntry):
         ai = None if acc_in is None else np.ascontiguousarray(acc_in.numpy()).copy()
         return torch.from_numpy(ref.reduce(np.stack(self.rows), self.ws, acc_in=ai, W=W))
 
+    def chainable(self):
+        return True
+
     def release(self):
         self.rows, self.ws = [], []
+
+
+class DrainedChainEntry(ChainOracleEntry):
+    """A rank whose rows were drained from +0 before the chain reached it
+    (the HIP entry's ring full): it cannot continue another rank's sum."""
+
+    def chainable(self):
+        return False
 
 
 def oracle_step(step, avg):

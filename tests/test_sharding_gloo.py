@@ -421,7 +421,7 @@ def test_client_sharded_round_loop(world, mode):
     """Each rank trains only its block of every round's sampled clients (5 of
     20 per round here), receives every message (the others' vectors as
     stand-ins), and the blocks are combined: the reference's own 5-round
-    FedAvg (lr 1.0 / 0.3), AdaBest, FedNova and FedDyn trajectories BITWISE
+    FedAvg (lr 1.0 / 0.3), FedNova and FedDyn trajectories BITWISE
     with the chain, within 1e-6 normwise with the all-reduce; scores equal
     on every rank."""
     import json
@@ -429,8 +429,11 @@ def test_client_sharded_round_loop(world, mode):
     from conftest import GOLDEN_DIR
 
     with open(os.path.join(GOLDEN_DIR, "rounds.json")) as f:
+        # AdaBest's clients read a running mean that every receive updates
+        # (adabest.py:76-80,167-169): refused under client sharding (below)
         runs = [r for r in json.load(f)["runs"]
-                if r.get("client", "synthetic") == "synthetic" and r["algorithm"] != "FedDF"]
+                if r.get("client", "synthetic") == "synthetic"
+                and r["algorithm"] not in ("FedDF", "AdaBest")]
     with np.load(os.path.join(GOLDEN_DIR, "rounds.npz"), allow_pickle=False) as z:
         arrays = {k: z[k] for k in z.files}
     with tempfile.TemporaryDirectory() as d:
@@ -560,14 +563,70 @@ def _client_extras_worker(rank, world, port, outdir):
         except RuntimeError as e:
             res["failure"] = "other: " + str(e)
 
-        # (3) FedDF keeps every client vector: refused on every rank
-        feddf = S.make_algorithm(training.FedDF)
-        alg = make(feddf)
+        # (3) AdaBest: a client's context (average_sample) depends on the
+        # earlier clients' receive_from_client -> refused on every rank
+        alg = make(S.make_algorithm(training.AdaBest))
         try:
             alg.train(rounds=0)
-            res["feddf"] = "ran"
-        except NotImplementedError as e:
-            res["feddf"] = str(e)
+            res["adabest"] = "ran"
+        except RuntimeError as e:
+            res["adabest"] = str(e)
+        # ... and runs when the check is off (the caller accepts round-start
+        # contexts): every rank still ends with the same model
+        alg = make(S.make_algorithm(training.AdaBest), check_client_context=False)
+        alg.train(rounds=1)
+        res["adabest_unchecked"] = alg.get_server_storage().read("cloud_params").detach().tolist()
+
+        # (6) a client that consumes Python random on rank 1 only: the next
+        # round's samples differ -> every rank raises, none hangs
+        def drawing(id, rounds, *a, _f=synth.send_to_server, **k):
+            if rank == 1:
+                random.random()
+            return _f(id, rounds, *a, **k)
+
+        alg = make(type("Drawing", (synth,), {"send_to_server": staticmethod(drawing)}))
+        try:
+            alg.train(rounds=S.ROUNDS)
+            res["desync"] = "ran"
+        except RuntimeError as e:
+            res["desync"] = str(e)[:60]
+
+        # (7) rank 1 drained rows from +0 before the chain reached it: the
+        # feasibility is agreed collectively, every rank raises, none hangs
+        from shard_oracle import DrainedChainEntry
+
+        def drained_factory(**kw):
+            return ClientShardedSerialAggregator(
+                entry_factory=DrainedChainEntry if rank == 1 else ChainOracleEntry,
+                step_impl=oracle_step, **kw)
+
+        random.seed(S.RANDOM_SEED)
+        torch.manual_seed(S.TORCH_SEED)
+        alg = synth(data_manager=S.FakeDataManager(), metric_logger=None,
+                    num_clients=S.NUM_CLIENTS, sample_scheme="uniform",
+                    sample_rate=S.SAMPLE_RATE, model_def=S.TinyModel, epochs=1,
+                    criterion_def="CrossEntropyScore", device="cpu",
+                    aggregator_factory=drained_factory)
+        try:
+            alg.train(rounds=0)
+            res["drained"] = "ran"
+        except RuntimeError as e:
+            res["drained"] = str(e)[:60]
+
+        # (8) stateful clients and a divergence: clients after the diverged
+        # one keep the storage they had before that round (the reference
+        # never trained them)
+        def stateful_diverging(id, rounds, storage, *a, _f=synth.send_to_server, **k):
+            msg = stateful(id, rounds, storage, *a, _f=_f, **k)
+            if rounds == 2 and id == sampled[2][1]:
+                msg["diverged"] = True
+            return msg
+
+        alg = make(type("StatefulDiverging", (synth,),
+                        {"send_to_server": staticmethod(stateful_diverging)}))
+        alg.train(rounds=S.ROUNDS)
+        res["div_count"] = {cid: alg._client_memory[cid].read("count") or 0
+                            for cid in range(S.NUM_CLIENTS)}
         with open(os.path.join(outdir, f"extras_rank{rank}.json"), "w") as f:
             json.dump(res, f)
     finally:
@@ -577,11 +636,13 @@ def _client_extras_worker(rank, world, port, outdir):
 def test_client_sharded_state_divergence_and_refusal():
     """Client storages written on one rank reach every rank (the next round
     may train that client elsewhere); a diverged client stops the whole
-    training on every rank at the same round with the same state; FedDF,
-    which keeps every client's vector, is refused with NotImplementedError
-    rather than run on stand-ins; with real local SGD (each rank drawing
-    its own random numbers) every rank still ends each round with the same
-    model."""
+    training on every rank at the same round with the same state, and the
+    clients after it keep their pre-round storage; AdaBest, whose clients'
+    context depends on the earlier clients of the round, is refused (and runs
+    with the check off); ranks whose client samples drift apart, or a rank
+    that cannot continue the chain, make every rank raise instead of hang;
+    with real local SGD (each rank drawing its own random numbers) every rank
+    still ends each round with the same model."""
     import json
 
     world = 2
@@ -602,4 +663,134 @@ def test_client_sharded_state_divergence_and_refusal():
         assert res[0]["count"][str(cid)] == len(times)
         assert res[0]["seen"][str(cid)] == [float(i) for i in times]
     assert res[0]["diverged_rounds"] == 2  # rounds 0 and 1 completed
-    assert "FedDF" in res[0]["feddf"] or "every client" in res[0]["feddf"]
+    assert "depend on each other" in res[0]["adabest"], res[0]["adabest"]
+    assert res[0]["desync"].startswith("the ranks of a client-sharded round sampled"), res[0]
+    assert res[0]["drained"].startswith("client_reduction='chain': a rank drained"), res[0]
+    # round 2 trained its clients up to the diverged one (position 1)
+    want = {cid: len([i for i, s in enumerate(sampled) if cid in s and
+                      (i < 2 or (i == 2 and s.index(cid) <= 1))]) for cid in range(20)}
+    assert {int(k): v for k, v in res[0]["div_count"].items()} == want
+
+
+# ---------------------------------------------------------------------------
+# FedDF under client-sharded rounds: the reference's own CNN rounds
+# ---------------------------------------------------------------------------
+def _feddf_worker(rank, world, port, mode, outdir):
+    import json
+    import random
+    from functools import partial
+
+    import torch.distributed as dist
+
+    from conftest import GOLDEN_DIR
+    from fedsim_amd import models
+    from fedsim_amd.distributed.centralized import training
+    from fedsim_amd.distributed.centralized.training import feddf
+    from fedsim_amd.sharding import ClientShardedSerialAggregator
+    from oracle import synthetic_fl as S
+    from shard_oracle import ChainOracleEntry, oracle_step
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with open(os.path.join(GOLDEN_DIR, "feddf_cnn.json")) as f:
+            G = json.load(f)
+        for run in G["runs"]:
+            record = []
+            orig = feddf.ShardedTeachers.mean_logits
+
+            def spy(self, x, _orig=orig):
+                out = _orig(self, x)
+                record.append(out.detach().cpu().numpy().copy())
+                return out
+
+            feddf.ShardedTeachers.mean_logits = spy
+            try:
+                cls = S.make_algorithm(training.FedDF)
+                dm = S.ImageDataManager(G["num_clients"], run["image_shape"], run["num_classes"],
+                                        G["valid_size"])
+                random.seed(S.RANDOM_SEED)
+                torch.manual_seed(S.TORCH_SEED)
+                alg = cls(data_manager=dm, metric_logger=None, num_clients=G["num_clients"],
+                          sample_scheme="uniform", sample_rate=G["sample_rate"],
+                          model_def=partial(getattr(models, run["model"]),
+                                            **run["model_kwargs"]),
+                          epochs=1, criterion_def="CrossEntropyScore",
+                          optimizer_def=partial(torch.optim.SGD, lr=G["lr"]), device="cpu",
+                          global_epochs=G["global_epochs"],
+                          aggregator_factory=partial(ClientShardedSerialAggregator, mode=mode,
+                                                     entry_factory=ChainOracleEntry,
+                                                     step_impl=oracle_step))
+                scores = alg.train(rounds=G["rounds"])
+            finally:
+                feddf.ShardedTeachers.mean_logits = orig
+            st = alg.get_server_storage()
+            np.savez(os.path.join(outdir, f"{run['id']}_rank{rank}.npz"),
+                     targets=np.stack(record),
+                     cloud=st.read("cloud_params").detach().numpy(),
+                     model=torch.nn.utils.parameters_to_vector(
+                         st.read("model").parameters()).detach().numpy())
+            with open(os.path.join(outdir, f"{run['id']}_rank{rank}.json"), "w") as f:
+                json.dump(dict(scores={k: float(v) for k, v in scores.items()},
+                               replay=st.read("teacher_replay")), f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(3, "chain"), (2, "allreduce")])
+def test_client_sharded_feddf_matches_reference(world, mode):
+    """FedDF with each rank training and replaying only its own clients'
+    teachers (K=4 per round over 2 / 3 ranks), the per-rank logit sums
+    combined by the round's aggregator (feddf.py:117-142): against the
+    reference's own SimpleCNN2(num_classes=100) / SimpleCNN FedDF rounds
+    (tests/golden/feddf_cnn.*).  chain: targets within 1e-5 (round 0) /
+    1e-4, cloud within 1e-4 normwise -- bitwise (cloud SHA-256, targets, scores)
+    on the host that made the goldens; allreduce (reordered sum): the same
+    normwise bounds.  Every rank ends with the same cloud and the same model
+    (the last teacher, broadcast from its rank)."""
+    import json
+
+    from conftest import GOLDEN_DIR
+    from oracle import synthetic_fl as S
+
+    with open(os.path.join(GOLDEN_DIR, "feddf_cnn.json")) as f:
+        G = json.load(f)
+    same_host = G.get("host") == S.host_signature()
+    with np.load(os.path.join(GOLDEN_DIR, "feddf_cnn.npz"), allow_pickle=False) as z:
+        golden = {k: z[k] for k in z.files}
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_feddf_worker, args=(world, _free_port(), mode, d), nprocs=world,
+                           join=True, start_method="spawn")
+        for run in G["runs"]:
+            rid = run["id"]
+            got = [dict(np.load(os.path.join(d, f"{rid}_rank{r}.npz"))) for r in range(world)]
+            meta = [json.load(open(os.path.join(d, f"{rid}_rank{r}.json")))
+                    for r in range(world)]
+            for r in range(1, world):
+                np.testing.assert_array_equal(bits(got[r]["cloud"]), bits(got[0]["cloud"]))
+                np.testing.assert_array_equal(bits(got[r]["model"]), bits(got[0]["model"]))
+                np.testing.assert_array_equal(bits(got[r]["targets"]), bits(got[0]["targets"]))
+                assert meta[r]["scores"] == meta[0]["scores"]
+            want_t = golden[f"{rid}/targets"]  # [rounds, batches, B, classes]
+            rounds, nb = want_t.shape[:2]
+            t = got[0]["targets"]
+            per_round = t.shape[0] // rounds
+            assert per_round in (nb, nb * G["global_epochs"]), t.shape
+            for rr in range(rounds):
+                for b in range(nb):
+                    g, w = t[rr * per_round + b].astype(np.float64), want_t[rr, b]
+                    err = np.linalg.norm(g - w) / np.linalg.norm(w)
+                    assert err <= (1e-5 if rr == 0 else 1e-4), (rid, rr, b, err)
+                    if mode == "chain" and same_host:
+                        np.testing.assert_array_equal(bits(t[rr * per_round + b]), bits(w))
+            cloud = got[0]["cloud"]
+            e = (np.linalg.norm(cloud[::G["stride"]].astype(np.float64)
+                                - golden[f"{rid}/cloud_sample"])
+                 / np.linalg.norm(golden[f"{rid}/cloud_sample"]))
+            assert e <= 1e-4, (rid, e)
+            if mode == "chain" and same_host:
+                assert V.sha256(cloud) == run["cloud_sha256"], rid
+                assert meta[0]["scores"] == run["scores"]
+            rep = meta[0]["replay"]
+            assert rep["teachers_total"] == 4 and rep["client_reduction"] == mode
+            assert sum(m["replay"]["teachers_local"] for m in meta) == 4

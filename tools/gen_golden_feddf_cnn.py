@@ -130,7 +130,97 @@ def run(FedDF, feddf_mod, model_cls, model_kw, shape, classes):
     return arrays, meta
 
 
+K1000 = 1000          # teachers of the single-batch case (the size FedDF is timed at)
+K1000_BATCH = 64      # one distillation batch
+K1000_SEED = 41       # oracle/vectors.teacher_vectors seed
+K1000_X_SEED = 90201  # the batch's input: V.gauss(seed, 64 * C*H*W)
+
+
+def k1000_input(shape):
+    n = K1000_BATCH * int(np.prod(shape))
+    return V.gauss(K1000_X_SEED, n).astype(np.float32).reshape(K1000_BATCH, *shape)
+
+
+def run_k1000(R, feddf_mod, model_cls, model_kw, shape):
+    """The reference's own teacher loop over K=1000 teachers on ONE batch:
+    FedDF.optimize (feddf.py:97-144) with global_epochs=1 and a one-batch
+    distillation split; its ``target_agg.get("target")`` (feddf.py:126) is
+    recorded.  The teachers are init cloud + seeded deltas
+    (oracle/vectors.teacher_vectors), so only the [64, classes] target and
+    hashes are stored."""
+    from torch.utils.data import DataLoader, TensorDataset
+
+    torch.manual_seed(S.TORCH_SEED)
+    model = model_cls(**model_kw)
+    init = torch.nn.utils.parameters_to_vector(model.parameters()).detach().numpy().copy()
+    x = torch.from_numpy(k1000_input(shape))
+    st = R["Storage"]()
+    cloud = torch.from_numpy(init.copy()).requires_grad_(True)
+    st.write("cloud_params", cloud)
+    st.write("model", model)
+    st.write("global_train_split", "valid")
+    st.write("global_dataloaders",
+             {"valid": DataLoader(TensorDataset(x, torch.zeros(K1000_BATCH, dtype=torch.long)),
+                                  batch_size=K1000_BATCH)})
+    st.write("global_epochs", 1)
+    st.write("optimizer", torch.optim.SGD([cloud], lr=LR))
+    st.write("lr_scheduler", None)
+    st.write("device", "cpu")
+    agg, app = R["SerialAggregator"](), R["AppendixAggregator"]()
+    agg.add("local_params", torch.from_numpy(init.copy()), 1)
+    sha = []
+    for t in V.teacher_vectors(init, K1000, K1000_SEED):
+        app.append("local_params", torch.from_numpy(t))
+        if len(sha) < 2 or len(sha) == K1000 - 1:
+            sha.append(V.sha256(t))
+        else:
+            sha.append(None)
+    targets = []
+    base_agg = feddf_mod.SerialAggregator
+
+    class Recording(base_agg):
+        def get(self, key, *a, **k):
+            v = super().get(key, *a, **k)
+            if key == "target":
+                targets.append(v.detach().clone().numpy())
+            return v
+
+    feddf_mod.SerialAggregator = Recording
+    try:
+        feddf_mod.FedDF.optimize(st, agg, app)
+    finally:
+        feddf_mod.SerialAggregator = base_agg
+    assert len(targets) == 1, len(targets)
+    return targets[0], dict(init_sha256=V.sha256(init), P=int(init.size),
+                            x_sha256=V.sha256(x.numpy()),
+                            teacher_sha256={str(k): s for k, s in enumerate(sha) if s})
+
+
+def main_k1000():
+    R = import_reference("/root/reference")
+    _stub_torchvision()
+    models = importlib.import_module("fedsim.models.simple_models")
+    feddf_mod = importlib.import_module("fedsim.distributed.centralized.training.feddf")
+    torch.set_num_threads(os.cpu_count() or 1)
+    manifest, arrays = [], {}
+    for rid, mname, mkw, shape, classes in RUNS:
+        target, meta = run_k1000(R, feddf_mod, getattr(models, mname), mkw, shape)
+        assert target.shape == (K1000_BATCH, classes)
+        arrays[f"{rid}/target"] = target
+        manifest.append(dict(id=rid, model=mname, model_kwargs=mkw, image_shape=list(shape),
+                             num_classes=classes, **meta))
+        print(rid, mname, meta["P"], float(np.linalg.norm(target.astype(np.float64))))
+    gd = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(gd, "feddf_k1000.json"), "w") as f:
+        json.dump(dict(generator="tools/gen_golden_feddf_cnn.py --k1000", K=K1000,
+                       batch=K1000_BATCH, teacher_seed=K1000_SEED, x_seed=K1000_X_SEED,
+                       torch_seed=S.TORCH_SEED, runs=manifest), f, indent=1)
+    np.savez_compressed(os.path.join(gd, "feddf_k1000.npz"), **arrays)
+
+
 def main():
+    if "--k1000" in sys.argv[1:]:
+        return main_k1000()
     import_reference("/root/reference")
     _stub_torchvision()
     models = importlib.import_module("fedsim.models.simple_models")

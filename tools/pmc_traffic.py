@@ -18,9 +18,12 @@ usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR --K 1000 --P 25000000
 """
 import argparse
 import csv
+import datetime
 import glob
+import hashlib
 import json
 import os
+import socket
 
 KERNEL = "k_reduce_vec"
 
@@ -39,6 +42,27 @@ def read_counter(d, name, match, tag=""):
     if not vals:
         raise SystemExit(f"no {name} rows for {match} in {files}")
     return vals
+
+
+def lib_md5(path):
+    """md5 of the profiled libfedagg.so: bench.py reports this summary's
+    traffic only for the same build (bench.load_pmc)."""
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def gpu_name(d):
+    """Agent name / id rocprofv3 recorded next to the counters, if any."""
+    for fn in glob.glob(os.path.join(d, "**", "*agent_info.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Agent_Type", row.get("Type", "")).upper().endswith("GPU"):
+                    return "%s (%s)" % (row.get("Marketing_Name", row.get("Name", "?")),
+                                        row.get("Name", "?"))
+    return None
 
 
 CALIB_BYTES = 8 << 30  # tools/pmc_calib.hip: bytes read / written per launch
@@ -65,6 +89,11 @@ def main():
                     help="dwords per lane of the kernel's client-row loads / result stores")
     ap.add_argument("--calib-fetch", default=None)
     ap.add_argument("--calib-write", default=None)
+    ap.add_argument("--lib", default=os.path.join(os.path.dirname(__file__), "..", "fedsim_amd",
+                                                  "libfedagg.so"),
+                    help="the library the profiled bench loaded (its md5 is the build id)")
+    ap.add_argument("--profile", default=None,
+                    help="where the summary is committed (profiles/<round>/), for provenance")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                   "pmc_traffic.json"))
     a = ap.parse_args()
@@ -94,6 +123,13 @@ def main():
         hbm_bytes_per_launch=fetch_b + write_b,
         alg_bytes_per_launch=alg,
         traffic_over_alg=(fetch_b + write_b) / alg,
+        source=dict(
+            lib_md5=lib_md5(a.lib),
+            profile=a.profile or os.path.relpath(os.path.abspath(a.fetch_dir)),
+            fetch_dir=a.fetch_dir, write_dir=a.write_dir,
+            host=socket.gethostname(), gpu=gpu_name(a.fetch_dir),
+            utc=datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+        ),
         corrections=("KiB->B x1024; FETCH_SIZE x fetch_factor, WRITE_SIZE x write_factor: "
                      "measured on tools/pmc_calib (known 8 GiB at this width)" if calib else
                      "KiB->B x1024; FETCH_SIZE x2 for 16B/lane streaming reads on gfx950 "
