@@ -317,6 +317,16 @@ class ShardedTeachers(object):
         s = self.agg.ordered_rows_sum(rows, self.owners, n)
         return self.agg.divide(s, self.K).view(shape).to(x.device)
 
+    def sync_student(self, cloud, optimizer) -> None:
+        """Every rank distilled the same student from the same targets, but
+        the student's GPU backward (MIOpen / rocBLAS) need not give the same
+        bits twice: rank 0's cloud and the optimizer state of it are
+        broadcast, so every rank starts the next round from one model."""
+        self.agg.broadcast_from(cloud.data, 0)
+        for t in optimizer.state.get(cloud, {}).values():
+            if isinstance(t, torch.Tensor) and t.dim() > 0:
+                self.agg.broadcast_from(t, 0)
+
     def load_last(self):
         """The model holds the last teacher afterwards, as after the
         reference's loop (feddf.py:122): broadcast from the rank holding it."""
@@ -405,6 +415,8 @@ class FedDF(FedAvg):
                         lr_scheduler.step()
                     ran = True
             if ran:
+                if isinstance(teachers, ShardedTeachers):
+                    teachers.sync_student(cloud_params, optimizer)
                 teachers.load_last()
             server_storage.write("teacher_replay", teachers.stats())
         return serial_aggregator.pop_all()
