@@ -23,7 +23,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
 
 # Must match include/fedagg.h
-ABI_VERSION = 2  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row)
+ABI_VERSION = 3  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
+#                 3: the rejected flat-load / LDS-weight flag bits refused
 FEDAGG_INIT = 0x1
 FEDAGG_FINALIZE = 0x2
 FEDAGG_NT = 0x4
@@ -31,8 +32,6 @@ FEDAGG_SCALAR = 0x8
 FEDAGG_UNROLL_SHIFT = 8
 FEDAGG_VPT_SHIFT = 12
 FEDAGG_BS_SHIFT = 14
-FEDAGG_FLAT = 0x10000
-FEDAGG_LDSW = 0x20000
 FEDAGG_MAP_SHIFT = 18
 FEDAGG_FAST = 0x200000
 FEDAGG_RELU = 0x400000

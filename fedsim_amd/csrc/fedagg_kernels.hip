@@ -67,17 +67,13 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // the grid more finely: +1.4 % at 1000 x 25 M, +1.6 % at 1000 x 199,210, even
 // at 1.09 M / 3.125 M (tools/sweep_variants.py, profiles/r01as/, r01at/;
 // 512 / 1024 lanes were 0.5 / 2 % slower than 256).
-#ifndef FEDAGG_NARROW_BLOCK  // build-variant knob for those measurements
-#define FEDAGG_NARROW_BLOCK 64
-#endif
-constexpr int kNarrowBlock = FEDAGG_NARROW_BLOCK;
+constexpr int kNarrowBlock = 64;
 // Tuned defaults (profiles/r01_*: K=1000 x P=25M sweep on MI355X).
 constexpr int kDefaultUnroll = 4;
 constexpr int kDefaultVptSel = 2;  // 2 float4 slots per lane
 constexpr int kDefaultBsSel = 1;   // blocked layout: 256-lane workgroups
 constexpr int kRowsUnroll = 4;     // row-pointer fused step (fedagg_reduce_step_rows_f32)
 constexpr int kRowsVpt = 2;
-constexpr int kWeightTile = 2048;  // FEDAGG_LDSW ablation: weights per LDS tile
 // Default column mapping = narrow (tools/sweep_mapping.py, tools/ab_mapping.py,
 // profiles/r01r/, r01t/, interleaved A/B on MI355X):
 //  * P < 2^20: one column per lane, U = 8.  The f32x4-slot kernels cannot fill
@@ -157,15 +153,6 @@ struct RowsBlockedBuf {
   }
 };
 
-struct RowsTable {
-  const float* const* rows;
-  __device__ __forceinline__ const char* row(int64_t k) const {
-    return reinterpret_cast<const char*>(rows[k]);
-  }
-  template <bool NT>
-  __device__ __forceinline__ f32x4 load4(int64_t k, uint32_t goff) const;
-};
-
 // Row-pointer table loaded with buffer instructions: row k's base pointer is a
 // wave-uniform scalar load from the table, turned into a buffer descriptor in
 // SGPRs, and the lane's column stays a 32-bit VGPR voffset, so the unrolled
@@ -206,11 +193,6 @@ template <bool NT>
 __device__ __forceinline__ f32x4 RowsBlocked::load4(int64_t k, uint32_t goff) const {
   return ld4<NT>(row(k), goff);
 }
-template <bool NT>
-__device__ __forceinline__ f32x4 RowsTable::load4(int64_t k, uint32_t goff) const {
-  return ld4<NT>(row(k), goff);
-}
-
 template <bool NT>
 __device__ __forceinline__ float ld1(const char* base, uint32_t off) {
   const float* p = reinterpret_cast<const float*>(base + off);
@@ -409,16 +391,10 @@ struct EpiStep {  // server step on the average, in registers
 //   [b*BS*VPT, (b+1)*BS*VPT); lane t of the block owns s = base + j*BS + t
 //   for j < VPT, so every wave-instruction touches 64 consecutive slots (1 KiB).
 // ---------------------------------------------------------------------------
-// Per-client weight sources: wave-uniform scalar loads (default) or an LDS
-// tile (ablation).
+// Per-client weights: wave-uniform scalar loads.
 struct WeightsScalar {
   const float* __restrict__ w;
   __device__ __forceinline__ float operator()(int64_t k) const { return w[k]; }
-};
-struct WeightsLds {
-  const float* wsh;
-  int64_t k0;
-  __device__ __forceinline__ float operator()(int64_t k) const { return wsh[k - k0]; }
 };
 
 // Rows kb..ke-1 in order, U rows of loads in flight before the in-order adds.
@@ -447,7 +423,7 @@ __device__ __forceinline__ void accumulate_rows(const Rows& rows, const Wf& wf, 
   }
 }
 
-template <int BS, int U, int VPT, bool NT, bool GUARD, bool LDSW, class Rows, class Epi>
+template <int BS, int U, int VPT, bool NT, bool GUARD, class Rows, class Epi>
 __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
                                                 const float* __restrict__ w,
                                                 int64_t B, int64_t nvec,
@@ -474,20 +450,9 @@ __device__ __forceinline__ void reduce_vec_body(const Rows& rows,
       a[j] = ld4<false>(reinterpret_cast<const char*>(acc_in), off[j]);
   }
 
-  if constexpr (LDSW) {
-    // Ablation (FEDAGG_LDSW): weights staged through LDS in tiles and read
-    // back as a same-address (broadcast) ds_read, instead of s_load.
-    __shared__ float wsh[kWeightTile];
-    for (int64_t k0 = 0; k0 < B; k0 += kWeightTile) {
-      const int64_t n = (B - k0) < kWeightTile ? (B - k0) : kWeightTile;
-      __syncthreads();
-      for (int64_t i = threadIdx.x; i < n; i += BS) wsh[i] = w[k0 + i];
-      __syncthreads();
-      accumulate_rows<U, VPT, NT>(rows, WeightsLds{wsh, k0}, k0, k0 + n, off, a);
-    }
-  } else {
-    accumulate_rows<U, VPT, NT>(rows, WeightsScalar{w}, 0, B, off, a);
-  }
+  // the per-client weight is wave-uniform: scalar loads (an LDS-staged
+  // variant measured no better, DESIGN §3, and was removed)
+  accumulate_rows<U, VPT, NT>(rows, WeightsScalar{w}, 0, B, off, a);
 
   if (flags & FEDAGG_FINALIZE) {
 #pragma unroll
@@ -513,7 +478,7 @@ __device__ __forceinline__ void reduce_scalar_cols(const Rows& rows,
   epi.one(col, a);
 }
 
-template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false, class Epi = EpiStore>
+template <int BS, int U, int VPT, bool NT, class Rows, class Epi = EpiStore>
 __global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
                                                        const float* __restrict__ w,
                                                        int64_t B, int64_t nvec,
@@ -523,9 +488,9 @@ __global__ __launch_bounds__(BS) void k_reduce_vec(Rows rows,
   const int64_t block_start = static_cast<int64_t>(blockIdx.x) * (BS * VPT);
   const int64_t block_end = block_start + BS * VPT;
   if (block_end <= nvec) {
-    reduce_vec_body<BS, U, VPT, NT, false, LDSW>(rows, w, B, nvec, acc_in, epi, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, false>(rows, w, B, nvec, acc_in, epi, W32, flags);
   } else if (block_start < nvec) {
-    reduce_vec_body<BS, U, VPT, NT, true, LDSW>(rows, w, B, nvec, acc_in, epi, W32, flags);
+    reduce_vec_body<BS, U, VPT, NT, true>(rows, w, B, nvec, acc_in, epi, W32, flags);
   }
   // The last block also owns the (P % 4) scalar tail columns.
   if (blockIdx.x == gridDim.x - 1 && static_cast<int>(threadIdx.x) < tail)
@@ -1145,7 +1110,7 @@ inline int elementwise_grid(int64_t n) {
   return static_cast<int>(g);
 }
 
-template <int BS, int U, int VPT, bool NT, class Rows, bool LDSW = false, class Epi = EpiStore>
+template <int BS, int U, int VPT, bool NT, class Rows, class Epi = EpiStore>
 hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
                       const float* acc_in, const Epi& epi, float W32, int flags,
                       hipStream_t s) {
@@ -1155,7 +1120,7 @@ hipError_t launch_vec(const Rows& rows, const float* w, int64_t B, int64_t P,
   // workgroup whose column span contains it (matters for RowsBlocked)
   int64_t grid = (nvec + (tail > 0 ? 1 : 0) + BS * VPT - 1) / (BS * VPT);
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows, LDSW, Epi>),
+  hipLaunchKernelGGL((k_reduce_vec<BS, U, VPT, NT, Rows, Epi>),
                      dim3(static_cast<unsigned>(grid)), dim3(BS), 0, s, rows, w, B, nvec, tail,
                      acc_in, epi, W32, flags);
   return hipGetLastError();
@@ -1231,8 +1196,7 @@ int check_reduce_args(const float* w, int64_t B, int64_t P, const float* acc_in,
   if (B > 0 && !w) return FEDAGG_EINVAL;
   if (!(flags & FEDAGG_INIT) && !acc_in) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_FINALIZE | FEDAGG_NT | FEDAGG_SCALAR | FEDAGG_UNROLL_MASK |
-                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_MAP_MASK |
-                FEDAGG_FAST))
+                FEDAGG_VPT_MASK | FEDAGG_BS_MASK | FEDAGG_MAP_MASK | FEDAGG_FAST))
     return FEDAGG_EINVAL;
   if (((flags & FEDAGG_MAP_MASK) >> FEDAGG_MAP_SHIFT) > 4) return FEDAGG_EINVAL;
   return 0;
@@ -1268,19 +1232,10 @@ int max_cols_per_lane(int64_t P, std::initializer_list<const void*> ptrs) {
 
 // Borrowed rows (pointer table) with two columns per lane read two pieces per
 // lane from P >= kRowsPiecesP on, with at most kRowsPiecesU rows in flight
-// (build knobs for the A/B in tools/ab_rows_variants.py).
-#ifndef FEDAGG_ROWS_PC
-#define FEDAGG_ROWS_PC 2
-#endif
-#ifndef FEDAGG_ROWS_PCU
-#define FEDAGG_ROWS_PCU 8
-#endif
-#ifndef FEDAGG_ROWS_PC_LOG2P
-#define FEDAGG_ROWS_PC_LOG2P 22
-#endif
-constexpr int kRowsPieces = FEDAGG_ROWS_PC;
-constexpr int kRowsPiecesU = FEDAGG_ROWS_PCU;
-constexpr int64_t kRowsPiecesP = int64_t(1) << FEDAGG_ROWS_PC_LOG2P;
+// (profiles/r01cf/).
+constexpr int kRowsPieces = 2;
+constexpr int kRowsPiecesU = 8;
+constexpr int64_t kRowsPiecesP = int64_t(1) << 22;
 
 template <int U, int VW, bool NT, class NR, class Epi>
 hipError_t launch_narrow_t(const NR& rows, const float* w, int64_t B, int64_t P,
@@ -1395,11 +1350,7 @@ hipError_t launch_splitk(const NR& rows, int S, const float* w, int64_t B, int64
 
 // Column-block widths the blocked kernels are built for (one workgroup's span
 // of the wide mapping; a multiple of a narrow workgroup's kNarrowBlock * 4 columns).
-#ifdef FEDAGG_ANY_C  // layout experiments (tools/ab_small_c.py): any power of two 128..16384
-inline bool valid_block_cols(int64_t C) { return C >= 128 && C <= 16384 && !(C & (C - 1)); }
-#else
 inline bool valid_block_cols(int64_t C) { return C == 1024 || C == 2048 || C == 4096; }
-#endif
 
 // Validate a server step's operands and pack them for EpiStep.
 int make_step(int algo, float coef, float* cloud, float* aux, float* avg_prev, float* buf,
@@ -1456,26 +1407,13 @@ hipError_t with_step(int algo, bool mom, const StepPtrs& sp, F&& f) {
 // chain per output, the bias added last).  Every teacher's weights are read
 // once per 64-row tile: a FedDF batch (64 samples) reads each teacher once.
 // ---------------------------------------------------------------------------
-#ifndef FEDAGG_TL_VEC  // 16-byte staging loads where aligned (A/B builds: 0 = off)
-#define FEDAGG_TL_VEC 1
-#endif
 constexpr int kTL_M = 64;  // output rows (samples) per workgroup
 constexpr int kTL_N = 64;  // output columns (features) per workgroup
 constexpr int kTL_K = 32;  // inputs per LDS stage
 constexpr int kTL_PAD = 1;
 
-#ifndef FEDAGG_TL_WPE  // waves per SIMD the Linear kernel is compiled for (A/B builds; 0: the
-#define FEDAGG_TL_WPE 0  // compiler's choice)
-#endif
-#ifndef FEDAGG_TL_BUF  // the buffer-descriptor Linear kernel where it applies (A/B builds: 0 = off)
-#define FEDAGG_TL_BUF 1
-#endif
-#ifndef FEDAGG_TL_WIDE_IN  // inputs above which a Linear layer counts as wide (see the launch)
-#define FEDAGG_TL_WIDE_IN 1024
-#endif
-#ifndef FEDAGG_TL_PAD_KB  // LDS reserved per workgroup of a wide layer: 4 per CU (A/B: 0 = none)
-#define FEDAGG_TL_PAD_KB 20
-#endif
+constexpr int64_t kTL_WideIn = 1024;  // inputs above which a Linear layer counts as wide
+constexpr size_t kTL_WidePadKB = 20;   // LDS reserved per workgroup of a wide layer: 4 per CU
 
 // XCD-aware order of a 1-D grid of teacher tiles (the 1-D form of
 // conv_tile_order below): launch index L runs on XCD L % 8, so in plain order
@@ -1484,21 +1422,13 @@ constexpr int kTL_PAD = 1;
 // tiles, a 0.8 MB input per teacher).  Renumbered, each XCD walks one
 // contiguous range of tiles, so a teacher's tiles share one L2.  Bijective;
 // placement only changes speed, never results.
-#ifndef FEDAGG_LINEAR_XCD_ORDER  // 0: plain dispatch order (A/B builds)
-#define FEDAGG_LINEAR_XCD_ORDER 1
-#endif
 __device__ __forceinline__ uint32_t xcd_tile_1d() {
   const uint32_t L = blockIdx.x;
-  if (!FEDAGG_LINEAR_XCD_ORDER) return L;
   const uint32_t n = gridDim.x, xcd = L & 7u, slot = L >> 3, q = n >> 3, r = n & 7u;
   return slot + (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q);
 }
 
-__global__ __launch_bounds__(256)
-#if FEDAGG_TL_WPE
-__attribute__((amdgpu_waves_per_eu(FEDAGG_TL_WPE, FEDAGG_TL_WPE)))
-#endif
-void k_teacher_linear(
+__global__ __launch_bounds__(256) void k_teacher_linear(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, int64_t M, int64_t in, int64_t out,
     float* __restrict__ y, int64_t n_tiles, int64_t m_tiles, int relu) {
@@ -1525,12 +1455,8 @@ void k_teacher_linear(
   // 16-byte loads when every row of x and of this teacher's W starts 16-B
   // aligned (workgroup-uniform): thread t owns inputs 4 (t % 8) .. + 3 of
   // rows t / 8 + 32 j; else one float per load as e = t + 256 j
-#if FEDAGG_TL_VEC
   const bool vec = (in % 4) == 0 && (reinterpret_cast<uintptr_t>(xk) % 16) == 0 &&
                    (reinterpret_cast<uintptr_t>(wk) % 16) == 0;
-#else
-  const bool vec = false;
-#endif
   auto fetch = [&](int64_t i0) {
     if (vec) {
 #pragma unroll
@@ -1739,15 +1665,11 @@ __global__ __launch_bounds__(256) void k_teacher_linear_buf(
 // read from HBM about once, and the partial cache lines two neighbouring
 // tiles write at an image boundary merge in one L2.  Bijective for any grid;
 // placement only changes speed, never results.
-#ifndef FEDAGG_CONV_XCD_ORDER  // 0: plain dispatch order (A/B builds)
-#define FEDAGG_CONV_XCD_ORDER 1
-#endif
 struct ConvTile {
   int x, y, z;
 };
 __device__ __forceinline__ ConvTile conv_tile_order() {
   const uint32_t gx = gridDim.x, gy = gridDim.y;
-  if (!FEDAGG_CONV_XCD_ORDER) return {int(blockIdx.x), int(blockIdx.y), int(blockIdx.z)};
   const uint32_t gxy = gx * gy, n = gxy * gridDim.z;
   const uint32_t L = blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z;
   const uint32_t xcd = L & 7u, slot = L >> 3, q = n >> 3, r = n & 7u;
@@ -1926,11 +1848,10 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
 constexpr int kTC_XPK_LDS = 14;  // LDS float index bits of a packed staging offset
 constexpr int kTC_XPK_GLB = 18;  // global float offset bits
 
-#ifndef FEDAGG_LDS_WPE  // waves per SIMD the chunked conv is compiled for (A/B builds; 4
-#define FEDAGG_LDS_WPE 3   // spills 57 VGPRs: SimpleCNN2 conv2 7.50 vs 6.92 ms, profiles/r02xi)
-#endif
+// 3 waves per SIMD (4 spill 57 VGPRs: SimpleCNN2 conv2 7.50 vs 6.92 ms,
+// profiles/r02xi)
 template <int KS, int CC, int XM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_LDS_WPE, FEDAGG_LDS_WPE))) void k_teacher_conv2d_lds(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_lds(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
     float* __restrict__ y, int relu) {
@@ -2127,13 +2048,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEDAGG_LDS_
 // (fedagg_conv_order 0, oracle ref_teacher_conv2d_f32 with cc = 0): a
 // trailing +0 term leaves a chain that never holds -0 unchanged.
 // ---------------------------------------------------------------------------
-#ifndef FEDAGG_FLAT_WAVES  // waves per workgroup of the flat conv, 64 output pixels each (A/B
-#define FEDAGG_FLAT_WAVES 4   // builds: 8 stages each image once per 512 pixels but runs two
-#endif                        // workgroups per CU; conv1 2.33 vs 2.13 ms, profiles/r02xf)
-constexpr int kFlatThreads = 64 * FEDAGG_FLAT_WAVES;
-#ifndef FEDAGG_FLAT_WPE  // waves per SIMD the flat conv is compiled for (A/B builds): 4 -> 3 lost
-#define FEDAGG_FLAT_WPE 5  // 10 % (r02x3); with the compact row staging 5 fit without spills
-#endif                     // (<= 96 VGPRs): SimpleCNN2 conv1 2.058 vs 2.217 ms (profiles/r03l); 6 spills
+// 4 waves per workgroup of the flat conv, 64 output pixels each (8 stage
+// each image once per 512 pixels but run two workgroups per CU: conv1 2.33
+// vs 2.13 ms, profiles/r02xf); compiled for 5 waves per SIMD (4 -> 3 lost 10 %,
+// r02x3; with the compact row staging 5 fit without spills in <= 96 VGPRs:
+// SimpleCNN2 conv1 2.058 vs 2.217 ms, profiles/r03l; 6 spill)
+constexpr int kFlatThreads = 64 * 4;
 // POOL: the 2 x 2 / stride 2 max pool (padding ppad = 0 or 1) that follows
 // the layer is fused into the store (FEDAGG_CONV_MAXPOOL2; SimpleCNN's
 // relu -> max_pool2d(2, 2, padding=1), simple_models.py:156-159).  The
@@ -2155,7 +2075,7 @@ __device__ __forceinline__ float pool_dpp_max(float m) {
 }
 
 template <int KS, int CI, int XM, bool HALF, bool POOL>
-__global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(FEDAGG_FLAT_WPE, FEDAGG_FLAT_WPE))) void k_teacher_conv2d_flat(
+__global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
     int nrows, float* __restrict__ y, int relu, int ppad) {
@@ -2499,17 +2419,13 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
     }
   }
   if (pool_pad >= 0) return false;  // the pool is fused by the flat kernel only
-#ifndef FEDAGG_CONV_CC2_XM16  // chunks of 2 channels where 4 would need 16 staging registers
-#define FEDAGG_CONV_CC2_XM16 1  // (SimpleCNN conv2, 32 ch at 14x14: whole teacher batch at
-#endif                          // K=1000 14.55 -> 13.97 ms, profiles/r02xa; 0 for A/B builds)
-#ifndef FEDAGG_CONV_XM12  // chunks of 4 channels with 12 staging registers where 8 do not
-#define FEDAGG_CONV_XM12 0  // suffice (A/B build knob)
-#endif
+  // chunks of 2 channels where 4 would need 16 staging registers (SimpleCNN
+  // conv2, 32 ch at 14x14: whole teacher batch at K=1000 14.55 -> 13.97 ms,
+  // profiles/r02xa)
   int cc = s.C >= 4 ? 4 : 2;
-  if (FEDAGG_CONV_CC2_XM16 && cc == 4 && cc * nslot * HW > (FEDAGG_CONV_XM12 ? 12 : 8) * 256)
-    cc = 2;
+  if (cc == 4 && cc * nslot * HW > 8 * 256) cc = 2;
   const int64_t xtot = cc * nslot * HW;
-  const int xm = xtot <= 8 * 256 ? 8 : (FEDAGG_CONV_XM12 && xtot <= 12 * 256) ? 12 : 16;
+  const int xm = xtot <= 8 * 256 ? 8 : 16;
   if (xtot > xm * 256) return false;
   if (nslot * cc * Hp * Wp >= (int64_t(1) << kTC_XPK_LDS)) return false;
   if (nslot * s.C * HW + cc * HW >= (int64_t(1) << kTC_XPK_GLB)) return false;
@@ -3073,9 +2989,6 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
   if (vw)
     return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B, P,
                                                 acc_in, out, W32, flags, s));
-  // buffer-descriptor loads unless asked for flat 64-bit addressing
-  if (flags & FEDAGG_FLAT)
-    return static_cast<int>(dispatch_reduce(RowsTable{rows}, w, B, P, acc_in, out, W32, flags, s));
   return static_cast<int>(dispatch_reduce(RowsTableBuf{rows, table_row_bytes(P)}, w, B, P, acc_in,
                                           out, W32, flags, s));
 }
@@ -3094,25 +3007,19 @@ int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const fl
   if (bs_sel == 0) bs_sel = kDefaultBsSel;
   hipError_t e;
   const bool region32 = Kcap * C * 4 < (int64_t(1) << 32);
-  const int vw = (flags & (FEDAGG_LDSW | FEDAGG_FLAT)) || !region32
-                     ? 0
-                     : narrow_vw(flags, P, B,
-                                 max_cols_per_lane(P, {out, (flags & FEDAGG_INIT) ? nullptr
-                                                                                 : acc_in}));
-  // buffer-descriptor path unless asked for flat loads or a block region is
-  // too large for a 32-bit descriptor range
-  const int S = region32 && !(flags & (FEDAGG_LDSW | FEDAGG_FLAT)) ? fast_split(flags, P) : 0;
+  const int vw = !region32 ? 0
+                           : narrow_vw(flags, P, B,
+                                       max_cols_per_lane(P, {out, (flags & FEDAGG_INIT) ? nullptr
+                                                                                       : acc_in}));
+  // buffer-descriptor path unless a block region is too large for a 32-bit
+  // descriptor range (then flat loads)
+  const int S = region32 ? fast_split(flags, P) : 0;
   if (S) {
     e = launch_splitk(NarrowBlocked{Xb, Kcap, C}, S, w, B, P, acc_in, EpiStore{out}, W32, flags,
                       s);
   } else if (vw) {
     e = launch_narrow_store(NarrowBlocked{Xb, Kcap, C}, vw, w, B, P, acc_in, out, W32, flags, s);
-  } else if (flags & FEDAGG_LDSW) {
-    // ablation: only the default configuration (C=4096, 256 lanes, U=4, nt)
-    if (C != 4096 || Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
-    e = launch_vec<256, 4, 4, true, RowsBlockedBuf, true>(RowsBlockedBuf{Xb, Kcap, C}, w, B, P,
-                                                          acc_in, EpiStore{out}, W32, flags, s);
-  } else if ((flags & FEDAGG_FLAT) || Kcap * C * 4 >= (int64_t(1) << 32)) {
+  } else if (!region32) {
     e = dispatch_blocked(RowsBlocked{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags, s);
   } else {
     e = dispatch_blocked(RowsBlockedBuf{Xb, Kcap, C}, C, bs_sel, w, B, P, acc_in, out, W32, flags,
@@ -3167,7 +3074,7 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
   const int64_t kchunk = kMaxGridX / per;
   // the buffer-descriptor kernel: every teacher's rows 16-B aligned, the
   // per-teacher extents within 32-bit byte offsets
-  const bool buf = FEDAGG_TL_BUF && (in % 4) == 0 && (x_kstride % 4) == 0 &&
+  const bool buf = (in % 4) == 0 && (x_kstride % 4) == 0 &&
                    (params_kstride % 4) == 0 && (w_off % 4) == 0 &&
                    (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
                    (reinterpret_cast<uintptr_t>(params) % 16) == 0 && M * in < (int64_t(1) << 29) &&
@@ -3179,7 +3086,7 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
       // workgroups per CU their 2048 concurrent row streams lose DRAM locality
       // (SimpleCNN's fc, in = 3136: 1049 vs 960 us for the generic kernel at
       // four per CU), so they reserve LDS for four per CU
-      const size_t pad = (in > FEDAGG_TL_WIDE_IN) ? size_t(FEDAGG_TL_PAD_KB) * 1024 : 0;
+      const size_t pad = (in > kTL_WideIn) ? kTL_WidePadKB * 1024 : 0;
       hipLaunchKernelGGL(k_teacher_linear_buf, dim3(static_cast<unsigned>(kn * per)), dim3(256), pad,
                          static_cast<hipStream_t>(stream), x + k0 * x_kstride, x_kstride,
                          params + k0 * params_kstride, params_kstride, w_off, b_off,
@@ -3597,7 +3504,7 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
   if (rc != 0) return rc;
   rc = check_reduce_args(w, B, P, acc_in, step->cloud, flags);
   if (rc != 0 || P == 0) return rc;
-  if (flags & (FEDAGG_FLAT | FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
+  if (flags & FEDAGG_SCALAR) return FEDAGG_EINVAL;
   if (B > Kcap || (B > 0 && !Xb)) return FEDAGG_EINVAL;
   if (!valid_block_cols(C)) return FEDAGG_EINVAL;
   if (Kcap * C * 4 >= (int64_t(1) << 32)) return FEDAGG_EINVAL;
@@ -3616,11 +3523,11 @@ int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, con
       return launch_narrow_step(NarrowBlocked{Xb, Kcap, C}, vw, w, B, P, acc_in, epi, W32, flags,
                                 s);
     switch (C) {
-      case 4096: return launch_vec<256, 4, 4, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
+      case 4096: return launch_vec<256, 4, 4, true, RowsBlockedBuf>(rows, w, B, P, acc_in,
                                                                           epi, W32, flags, s);
-      case 2048: return launch_vec<256, 2, 2, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
+      case 2048: return launch_vec<256, 2, 2, true, RowsBlockedBuf>(rows, w, B, P, acc_in,
                                                                           epi, W32, flags, s);
-      case 1024: return launch_vec<256, 2, 1, true, RowsBlockedBuf, false>(rows, w, B, P, acc_in,
+      case 1024: return launch_vec<256, 2, 1, true, RowsBlockedBuf>(rows, w, B, P, acc_in,
                                                                           epi, W32, flags, s);
       default: return hipErrorInvalidValue;
     }
@@ -3641,13 +3548,13 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   if (rc != 0) return rc;
   rc = check_reduce_args(w, B, P, acc_in, step->cloud, flags);
   if (rc != 0 || P == 0) return rc;
-  if (flags & (FEDAGG_LDSW | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
+  if (flags & FEDAGG_SCALAR) return FEDAGG_EINVAL;
   if (B > 0 && !rows) return FEDAGG_EINVAL;
   if (!step_aligned(sp) || (!(flags & FEDAGG_INIT) && !aligned16(acc_in))) return FEDAGG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   // the rows path's default configuration (256 lanes, kRowsVpt float4 slots
   // per lane, U = kRowsUnroll); the rows are the caller's separate
-  // allocations, read through buffer descriptors unless FEDAGG_FLAT
+  // allocations, read through buffer descriptors
   const bool nt = (flags & FEDAGG_NT) != 0;
   if (!row_fits_descriptor(P)) {  // P = 2^30: flat loads, one column per lane
     hipError_t e = with_step(step->algo, mom, sp, [&](auto epi) {
@@ -3671,14 +3578,13 @@ int fedagg_reduce_step_rows_f32(const float* const* rows, const float* w, int64_
   auto go = [&](const auto& tab) {
     using T = std::decay_t<decltype(tab)>;
     return with_step(step->algo, mom, sp, [&](auto epi) {
-      return nt ? launch_vec<kBlock, kRowsUnroll, kRowsVpt, true, T, false>(tab, w, B, P, acc_in,
+      return nt ? launch_vec<kBlock, kRowsUnroll, kRowsVpt, true, T>(tab, w, B, P, acc_in,
                                                                           epi, W32, flags, s)
-                : launch_vec<kBlock, kRowsUnroll, kRowsVpt, false, T, false>(
+                : launch_vec<kBlock, kRowsUnroll, kRowsVpt, false, T>(
                       tab, w, B, P, acc_in, epi, W32, flags, s);
     });
   };
-  hipError_t e = (flags & FEDAGG_FLAT) ? go(RowsTable{rows})
-                                       : go(RowsTableBuf{rows, table_row_bytes(P)});
+  hipError_t e = go(RowsTableBuf{rows, table_row_bytes(P)});
   if (e == hipErrorInvalidValue) return FEDAGG_EINVAL;
   return static_cast<int>(e);
 }

@@ -40,12 +40,10 @@ def fl32(x) -> float:
 
 
 def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
-                 flat: bool = False, ldsw: bool = False, mapping: str = "auto",
-                 fast: bool = False) -> int:
+                 mapping: str = "auto", fast: bool = False) -> int:
     """Kernel tuning bits (include/fedagg.h): k-unroll, float4 slots per lane
     (row-major / pointer-table layouts), non-temporal loads, the workgroup
-    size of the column-blocked layout, flat (instead of buffer-descriptor)
-    loads for it, and the column mapping (``"auto"``, ``"wide"`` = f32x4
+    size of the column-blocked layout, and the column mapping (``"auto"``, ``"wide"`` = f32x4
     slots, ``"narrow1"`` / ``"narrow2"`` / ``"narrow4"`` = one / two / four
     columns per lane).
     ``fast``: FEDAGG_FAST, the reordered split-K mode for small P (normwise
@@ -56,7 +54,6 @@ def tuning_flags(unroll: int = 0, vpt: int = 0, nt: bool = False, bs: int = 0,
     bsel = {0: 0, 256: 1, 512: 2, 1024: 3}[bs]
     return ((sel << _native.FEDAGG_UNROLL_SHIFT) | (vsel << _native.FEDAGG_VPT_SHIFT)
             | (bsel << _native.FEDAGG_BS_SHIFT) | (FEDAGG_NT if nt else 0)
-            | (_native.FEDAGG_FLAT if flat else 0) | (_native.FEDAGG_LDSW if ldsw else 0)
             | (msel << _native.FEDAGG_MAP_SHIFT) | (_native.FEDAGG_FAST if fast else 0))
 
 
@@ -804,7 +801,6 @@ def reduce_rows_step(
     W: Optional[float] = None,
     nt: bool = True,
     table: Optional[torch.Tensor] = None,
-    flat: bool = False,
     mapping: str = "auto",
     unroll: int = 0,
     checked: bool = False,
@@ -813,8 +809,7 @@ def reduce_rows_step(
     """reduce_rows(rows, ..., out=avg) then step.apply(avg), fused into one
     pass over the caller's own client tensors (fedagg_reduce_step_rows_f32):
     the zero-copy round of HBM-resident client vectors.  Returns step.cloud.
-    ``flat`` selects 64-bit flat loads instead of per-row buffer descriptors
-    (ablation; same arithmetic).  ``checked``: the caller has already
+    ``checked``: the caller has already
     validated every row (the aggregator does at ``add``), skip the per-row
     checks."""
     _require_hip_f32(w32, "w32")
@@ -831,7 +826,7 @@ def reduce_rows_step(
         raise ValueError("w32 too short")
     if not step.aligned():
         raise ValueError("every server-step operand must be 16-B aligned")
-    f = (FEDAGG_NT if nt else 0) | tuning_flags(flat=flat, mapping=mapping, unroll=unroll) | flags
+    f = (FEDAGG_NT if nt else 0) | tuning_flags(mapping=mapping, unroll=unroll) | flags
     if acc_in is None:
         f |= FEDAGG_INIT
     else:

@@ -58,8 +58,10 @@ extern "C" {
 
 /* 1: round-1 reduce / pack / step entry points; 2: + the FedDF teacher
    (linear, conv2d, pad-LRN-maxpool) and slab-row (pack_segments, unpack_row)
-   entry points and their structs */
-#define FEDAGG_ABI_VERSION 2
+   entry points and their structs; 3: flag bits 0x10000 / 0x20000 (the
+   flat-load and LDS-weight A/B switches, measured and rejected) are no
+   longer accepted (FEDAGG_EINVAL) */
+#define FEDAGG_ABI_VERSION 3
 
 /* flags for the reduce entry points */
 #define FEDAGG_INIT      0x1  /* ignore acc_in: start from +0.0f (first batch of a round) */
@@ -77,13 +79,10 @@ extern "C" {
  * 2 = 512, 3 = 1024 lanes (float4 slots per lane = C / (4 * lanes)) */
 #define FEDAGG_BS_SHIFT 14
 #define FEDAGG_BS_MASK  0xC000
-/* blocked layout: use flat global loads instead of buffer-descriptor loads
- * (A/B measurement switch; also taken automatically when a column block's
- * region is >= 4 GiB) */
-#define FEDAGG_FLAT     0x10000
-/* ablation: stage the per-client weights through LDS tiles instead of reading
- * them with wave-uniform scalar loads (same results; A/B measurement switch) */
-#define FEDAGG_LDSW     0x20000
+/* bits 16..17 are reserved (rejected).  The blocked layout reads through
+ * buffer descriptors, and falls back to flat global loads by itself when a
+ * column block's region is >= 4 GiB; per-client weights are wave-uniform
+ * scalar loads. */
 /* bits 18..20: column mapping of the reduce kernels.  An in-order per-column
  * sum is parallel over columns only, so at small P the f32x4-slot ("wide")
  * kernels leave CUs idle (P = 199,210 is 778 waves).  0 = library default
@@ -426,7 +425,7 @@ typedef struct fedagg_step_args {
  * Flags: FEDAGG_INIT / FEDAGG_FINALIZE as for the reduce; the column-mapping
  * bits and, for the narrow mapping, the unroll selector apply (the wide
  * mapping uses its per-C default configuration, non-temporal loads).
- * FEDAGG_FLAT / FEDAGG_LDSW / FEDAGG_SCALAR are rejected. Every [P] operand must be 16-byte aligned, and a
+ * FEDAGG_SCALAR is rejected. Every [P] operand must be 16-byte aligned, and a
  * column block's region (Kcap * C * 4 bytes) must be < 4 GiB.
  */
 int fedagg_reduce_step_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,

@@ -301,5 +301,24 @@ def test_stale_library_fails_with_the_version_message(tmp_path, monkeypatch):
     subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
     monkeypatch.setattr(_native, "LIB_PATH", str(so))
     monkeypatch.setattr(_native, "_lib", None)
-    with pytest.raises(_native.FedAggError, match="ABI version 1, this package needs 2"):
+    with pytest.raises(_native.FedAggError, match="ABI version 1, this package needs %d" % _native.ABI_VERSION):
         _native.load()
+
+
+def test_rejected_ab_flag_bits_are_gone():
+    """The flat-load / LDS-weight A/B switches (flag bits 0x10000 / 0x20000,
+    measured and rejected) are no longer part of the ABI: the
+    header reserves the bits and the Python side no longer names them."""
+    import re
+
+    from fedsim_amd import _native, ops
+
+    hdr = open(os.path.join(REPO, "include", "fedagg.h")).read()
+    assert not re.search(r"#define FEDAGG_(FLAT|LDSW)\b", hdr)
+    assert not hasattr(_native, "FEDAGG_FLAT") and not hasattr(_native, "FEDAGG_LDSW")
+    import inspect
+
+    assert "flat" not in inspect.signature(ops.tuning_flags).parameters
+    src = open(os.path.join(REPO, "fedsim_amd", "csrc", "fedagg_kernels.hip")).read()
+    # no build-variant knob of a finished experiment is left in the kernels
+    assert not re.search(r"^\s*#\s*if(n?def)?\b", src, re.M), "A/B build knobs in the kernels"

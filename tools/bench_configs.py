@@ -48,7 +48,7 @@ def gpu_time(fn, steps):
     """Median time of one isolated call between two HIP events on the current
     stream, synchronized each time: includes the launch latency of an idle
     GPU, which back-to-back calls (the wall-clock rate) overlap.  Kernel-only
-    times come from rocprofv3 or tools/sweep_variants.py."""
+    times come from rocprofv3."""
     ms = []
     for _ in range(steps):
         e0 = torch.cuda.Event(enable_timing=True)

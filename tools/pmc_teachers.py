@@ -1,6 +1,6 @@
 """HBM traffic of the FedDF teacher kernels from rocprofv3 FETCH_SIZE /
 WRITE_SIZE passes over tools/ab_teacher_conv.py (SimpleCNN2 layers, K=500,
-B=64; tools/gpu_r02pmc.sh), corrected by the per-box calibration passes
+B=64; tools/gpu_run.sh (pmc / sq steps; the round-2 script is in git history)), corrected by the per-box calibration passes
 over tools/pmc_calib (8 GiB read / written once per kernel, so factor =
 8 GiB / counter bytes; MI355X_MICROARCH.md: counters in KiB, FETCH_SIZE
 half of a streaming read on gfx950).  Algorithmic bytes per launch: the

@@ -1,4 +1,4 @@
-"""Per-kernel SQ counter summary of tools/gpu_r03sq.sh's two rocprofv3 --pmc
+"""Per-kernel SQ counter summary of tools/gpu_run.sh sq=<script>'s two rocprofv3 --pmc
 passes (mean over each kernel's launches, counters summed over the pass'
 rows of one dispatch), with the derived fractions used in DESIGN §3:
 
@@ -57,7 +57,7 @@ def main():
         if m.get("SQ_INSTS_MFMA"):
             m["valu_per_mfma"] = m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"]
         res[k] = m
-    json.dump(dict(source="tools/gpu_r03sq.sh (rocprofv3 --pmc, two passes) over "
+    json.dump(dict(source="tools/gpu_run.sh sq= (rocprofv3 --pmc, two passes) over "
                           "tools/ab_teacher_conv.py --K 500; tools/sq_summary.py",
                    kernels=res), open(out, "w"), indent=1)
     for k, m in res.items():
