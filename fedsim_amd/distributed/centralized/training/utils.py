@@ -120,9 +120,12 @@ def _handed_over(t: torch.Tensor) -> bool:
 
 
 def _would_borrow(aggregator, t) -> bool:
+    """The aggregator reads ``t`` after add returns: an HBM vector borrowed
+    in place, or a host vector staged by the ingest worker while the next
+    client trains (aggregators._Ingest.put_async)."""
     opts = getattr(aggregator, "_opts", None)
     return (isinstance(aggregator, _DeviceSerialAggregator) and opts is not None
-            and opts.borrow and isinstance(t, torch.Tensor) and t.device.type == "cuda")
+            and opts.borrow and isinstance(t, torch.Tensor))
 
 
 def pop_average(aggregator, key="local_params") -> torch.Tensor:

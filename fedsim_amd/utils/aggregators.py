@@ -31,6 +31,7 @@ from __future__ import annotations
 import os
 import struct
 from collections import deque
+from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Dict, List, Optional
 
 import torch
@@ -89,7 +90,18 @@ class _Ingest(object):
     one descriptor per C-float segment: at C = 1024 (P < 8 M) that ran at
     2 GB/s, against PCIe's 55 for the whole vector.  A slot is reused only
     after its previous copies have completed.  One ring per device is shared
-    by all aggregators (the round driver makes a new one every round)."""
+    by all aggregators (the round driver makes a new one every round).
+
+    Every put runs on ONE worker thread (in submission order, so the slots
+    and the copy stream see one sequence).  ``put`` waits for it: the
+    snapshot is taken when add returns, as the reference's clone.
+    ``put_async`` does not: for a host vector the client handed over (the
+    round driver's borrowing aggregator, training/utils.py ``_handed_over``),
+    the pageable-to-pinned copy and the DMA then run while the next client
+    trains instead of between the two clients (tools/bench_host_rounds.py:
+    0.2-1.5 ms per client on the critical path otherwise).  A handed-over
+    vector changed in place before its copy ran is caught by its version
+    counter and raised at the round's reduction."""
 
     def __init__(self, dev: torch.device, nslots: int = _STAGING_SLOTS):
         self.dev = dev
@@ -98,6 +110,15 @@ class _Ingest(object):
         self.dbufs: List[Optional[torch.Tensor]] = [None] * nslots
         self.events: List[Optional[torch.cuda.Event]] = [None] * nslots
         self.i = 0
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedsim-ingest",
+                                       initializer=torch.cuda.set_device, initargs=(dev,))
+
+    def put(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None):
+        return self.pool.submit(self._put, src, Xb, r, wait_event, None).result()
+
+    def put_async(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None) -> Future:
+        """Future of put's event; ``src`` must not change until it resolves."""
+        return self.pool.submit(self._put, src, Xb, r, wait_event, src._version)
 
     @staticmethod
     def _slot(bufs, i, P, **kw):
@@ -107,7 +128,12 @@ class _Ingest(object):
             bufs[i] = buf
         return buf[:P]
 
-    def put(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None):
+    def _put(self, src, Xb, r, wait_event, version):
+        if version is not None and src._version != version:
+            raise RuntimeError(
+                "a host client tensor was modified in place after SerialAggregator.add(); "
+                "an aggregator created with borrow=True copies it after add returns (use "
+                "borrow=False to snapshot it at add time)")
         i = self.i % len(self.events)
         self.i += 1
         if self.events[i] is not None:
@@ -127,7 +153,7 @@ class _Ingest(object):
         ev = torch.cuda.Event()
         ev.record(self.stream)
         self.events[i] = ev
-        if host is src:
+        if host is src and version is None:
             # the snapshot is complete once the DMA is: the caller may reuse
             # its pinned buffer after add returns
             ev.synchronize()
@@ -227,7 +253,14 @@ class _DeviceEntry(_TensorEntry):
         self.wait_before_copy = None
 
     # -- ring management -----------------------------------------------------
+    def _copies_issued(self) -> None:
+        """Host rows still being staged by the ingest worker have been issued
+        on its copy stream (copy_event is then their event)."""
+        if isinstance(self.copy_event, Future):
+            self.copy_event = self.copy_event.result()  # raises a modified-tensor error
+
     def _alloc(self, rows: int) -> None:
+        self._copies_issued()
         if self.slab is not None:
             self.rows.release(self.slab)
         self.slab = torch.empty((self.nblk, rows, self.C), dtype=torch.float32, device=self.dev)
@@ -272,6 +305,10 @@ class _DeviceEntry(_TensorEntry):
 
     def release(self) -> None:
         """Drop the slab; SlabRows still alive keep a copy of their row."""
+        self._copies_issued()
+        if self.copy_event is not None:  # the slab is read by the copy stream until then
+            self.copy_event.synchronize()
+            self.copy_event = None
         if self.slab is not None:
             self.rows.release(self.slab)
         self.slab = None
@@ -324,6 +361,12 @@ class _DeviceEntry(_TensorEntry):
             if src.device != self.dev:
                 src = src.to(self.dev)
             ops.pack_row(src.contiguous(), self.slab, r)  # D2D on the compute stream
+        elif self.borrow and src.is_contiguous():
+            # handed over (serial_aggregation clones otherwise): copied while
+            # the next client trains
+            self.copy_event = self.agg._ingest(self.dev).put_async(
+                src, self.slab, r, wait_event=self.wait_before_copy)
+            self.wait_before_copy = None
         else:
             self.copy_event = self.agg._ingest(self.dev).put(
                 src.contiguous(), self.slab, r, wait_event=self.wait_before_copy)
@@ -381,6 +424,7 @@ class _DeviceEntry(_TensorEntry):
             if final_W is not None and self.acc is not None:
                 ops.finalize(self.acc, final_W, out=self.acc)
             return
+        self._copies_issued()
         if self.copy_event is not None:
             cur.wait_event(self.copy_event)
             self.copy_event = None

@@ -33,3 +33,55 @@ def aggregate_round(rows: Sequence[torch.Tensor], weights: Sequence, ret_sum: bo
     if cur_w == 0:
         return sum_v
     return sum_v / cur_w
+
+
+class ReferenceSerialAggregator(object):
+    """The reference's SerialAggregator restated on torch CPU
+    (fedsim/utils/aggregators.py:11-144): per key, ``value * weight`` added to
+    the running sum (first add: ``0 + tensor``), the Python weight sum, and
+    ``sum / weight`` on get / pop (the raw sum for a zero / None weight).
+    TEST / MEASUREMENT INFRASTRUCTURE: the reference leg of
+    tools/bench_host_rounds.py."""
+
+    def __init__(self) -> None:
+        self._members = dict()
+
+    def add(self, key, value, weight=None):
+        new_v = value * weight if weight is not None else value
+        sum_v, cur_w = self._members.get(key, (0, 0))
+        self._members[key] = (sum_v + new_v, cur_w + weight)
+
+    def get(self, key):
+        if key not in self._members:
+            raise Exception(f"{key} is not in the aggregator")
+        v, w = self._members[key]
+        if w is None or w == 0:
+            return v
+        return v / w
+
+    def get_sum(self, key):
+        if key not in self._members:
+            raise Exception(f"{key} is not in the aggregator")
+        return self._members[key][0]
+
+    def get_weight(self, key):
+        if key not in self._members:
+            raise Exception(f"{key} is not in the aggregator")
+        return self._members[key][1]
+
+    def keys(self):
+        return self._members.keys()
+
+    def pop(self, key):
+        v = self.get(key)
+        del self._members[key]
+        return v
+
+    def items(self):
+        return {k: self.get(k) for k in self._members}.items()
+
+    def pop_all(self):
+        return {k: self.pop(k) for k in list(self._members)}
+
+    def __contains__(self, key):
+        return key in self._members

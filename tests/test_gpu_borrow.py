@@ -403,3 +403,67 @@ def test_client_reusing_its_buffer_matches_reference(dev):
     assert entry.borrowed[1][0].data_ptr() != kept.data_ptr()
     kept.fill_(5.0)  # the caller still owns it and may change it
     assert torch.equal(agg.pop("local_params"), torch.ones(4096, device=dev))
+
+
+def test_handed_over_host_rows_are_staged_after_add(dev):
+    """borrow=True with host vectors (the round driver's aggregator under
+    device="cpu"): each handed-over vector is copied into pinned staging and
+    DMA'd by the ingest worker after add returns (while the next client
+    trains), in arrival order, interleaved with HBM rows; the round is the
+    oracle's bit for bit."""
+    from fedsim_amd.utils import SerialAggregator
+
+    K, P = 23, 199_210
+    X = V.client_rows("realistic", K, P, 8)
+    w = V.client_weights("fedavg", K, 8)
+    agg = SerialAggregator(borrow=True, max_rows=5)
+    for k in range(K):
+        src = torch.from_numpy(X[k].copy())
+        if k % 5 == 4:
+            src = src.to(dev)
+        agg.add("p", src, w[k])
+        del src
+    out = agg.pop("p")
+    assert out.device.type == "cpu"
+    np.testing.assert_array_equal(bits(out.numpy()), bits(ref.reduce(X, w, W=sum(w))))
+
+
+def test_handed_over_host_row_mutated_in_place_raises(dev):
+    """A handed-over host vector changed in place before the ingest worker
+    copied it is refused at the reduction (held back here so the change comes
+    first: a change racing the copy itself is the caller's contract breach,
+    as for borrowed HBM rows)."""
+    import threading
+
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _ingest_for
+
+    agg = SerialAggregator(borrow=True)
+    gate = threading.Event()
+    _ingest_for(dev).pool.submit(gate.wait)  # the worker is busy until released
+    t = torch.ones(1 << 20)
+    agg.add("p", t, 1)
+    t.mul_(2)
+    gate.set()
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.pop("p")
+
+
+def test_host_client_keeping_its_vector_is_cloned(dev):
+    """serial_aggregation under the borrowing aggregator: a host vector the
+    client still references is cloned (the reference's snapshot), so changing
+    it after receive_from_client does not change the round."""
+    from fedsim_amd.distributed.centralized.training.utils import serial_aggregation
+    from fedsim_amd.utils import SerialAggregator, Storage
+
+    K, P = 6, 65_537
+    X = V.client_rows("realistic", K, P, 9)
+    w = V.client_weights("fedavg", K, 9)
+    agg = SerialAggregator(borrow=True)
+    kept = []
+    for k, msg in enumerate(V.client_messages(X, w)):
+        kept.append(msg["local_params"])  # the client keeps its tensor
+        assert serial_aggregation(Storage(), k, msg, "train", agg)
+        kept[-1].fill_(float("nan"))
+    out = agg.pop("local_params")
+    np.testing.assert_array_equal(bits(out.numpy()), bits(ref.reduce(X, w, W=sum(w))))

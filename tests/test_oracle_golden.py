@@ -119,3 +119,23 @@ def test_oracle_edge_cases():
         _, _, _, ok = ref.accepted(c["weights"], diverged)
         assert not ok and c["ok"][-1] is False and len(c["ok"]) == c["diverged_at"] + 1
     assert by_id
+
+
+@pytest.mark.parametrize("case", [c for c in PARAM_CASES if c["P"] <= 70_000][:40],
+                         ids=lambda c: c["id"])
+def test_reference_aggregator_restatement_matches_reference(case, golden):
+    """oracle.reference_loop.ReferenceSerialAggregator (the host leg of
+    tools/bench_host_rounds.py) gives the reference's own sum and average."""
+    import torch
+
+    from oracle.reference_loop import ReferenceSerialAggregator
+
+    _, arrays = golden
+    X = _inputs(case)
+    agg = ReferenceSerialAggregator()
+    for k, w in enumerate(case["weights"]):
+        if w > 0:
+            agg.add("p", torch.from_numpy(X[k].copy()).clone(), w)
+    _check(case, arrays, "sum", agg.get_sum("p").numpy())
+    _check(case, arrays, "avg", agg.pop("p").numpy())
+    assert "p" not in agg
