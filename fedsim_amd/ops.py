@@ -789,7 +789,12 @@ def reduce_blocked_step(
 def row_table(rows: Sequence[torch.Tensor], device: torch.device) -> torch.Tensor:
     """Device int64 table of the rows' data pointers (one pinned H2D copy,
     stream-ordered on the current stream)."""
-    host = torch.tensor([r.data_ptr() for r in rows] or [0], dtype=torch.int64).pin_memory()
+    return row_table_from_ptrs([r.data_ptr() for r in rows], device)
+
+
+def row_table_from_ptrs(ptrs: Sequence[int], device: torch.device) -> torch.Tensor:
+    """row_table of pointers collected beforehand (as rows arrive)."""
+    host = torch.tensor(list(ptrs) or [0], dtype=torch.int64).pin_memory()
     return host.to(device, non_blocking=True)
 
 
