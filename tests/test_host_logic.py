@@ -350,3 +350,53 @@ def test_feddf_target_reuse_conditions():
     assert not _pure_forward(drop)
     drop.eval()
     assert _pure_forward(drop)
+
+
+def test_client_context_fingerprint():
+    """The plain-data image of a send_to_client message that client-sharded
+    rounds compare (centralized_fl_algorithm._context_fingerprint): exact
+    floats (hex), small tensors by value, models and large tensors skipped."""
+    import math
+
+    import numpy as np
+    import torch
+
+    from fedsim_amd.distributed.centralized.centralized_fl_algorithm import (
+        _context_fingerprint)
+
+    model = torch.nn.Linear(3, 2)
+    a = _context_fingerprint(dict(model=model, average_sample=0.1, mu=0.01, n=3,
+                                  t=torch.tensor([1.0, 2.0]), big=torch.zeros(100),
+                                  s="x", np=np.float32(0.5), none=None, tup=(1, 2.0)))
+    assert set(a) == {"average_sample", "mu", "n", "t", "s", "np", "none", "tup"}
+    b = _context_fingerprint(dict(model=torch.nn.Linear(3, 2), average_sample=0.1, mu=0.01,
+                                  n=3, t=torch.tensor([1.0, 2.0]), big=torch.ones(100), s="x",
+                                  np=np.float32(0.5), none=None, tup=(1, 2.0)))
+    assert a == b  # models and big tensors do not take part
+    c = _context_fingerprint(dict(average_sample=math.nextafter(0.1, 1.0)))
+    assert c["average_sample"] != a["average_sample"]  # one ulp is a difference
+    assert _context_fingerprint(dict(x=float("nan"))) == _context_fingerprint(dict(x=float("nan")))
+    assert _context_fingerprint(None) is None
+
+
+def test_changed_client_storage_keys():
+    """Only the client-storage entries a round wrote are shared across ranks:
+    rebound entries, tensors changed in place, and mutable objects."""
+    import torch
+
+    from fedsim_amd.distributed.centralized.centralized_fl_algorithm import (
+        _changed_keys, _storage_state)
+    from fedsim_amd.utils import Storage
+
+    st = Storage()
+    h = torch.zeros(4)
+    st.write("h", h)
+    st.write("last_round", 2)
+    st.write("same", torch.ones(2))
+    st.write("d", {"a": 1})
+    state = _storage_state(st)
+    assert _changed_keys(st, state) == ["d"]  # a dict may change in place
+    h.add_(1)  # in place: its version counter moves
+    st.write("last_round", 3)
+    st.write("new", 5)
+    assert sorted(_changed_keys(st, state)) == ["d", "h", "last_round", "new"]
