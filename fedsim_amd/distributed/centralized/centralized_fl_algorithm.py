@@ -203,13 +203,13 @@ class CentralFLAlgorithm(object):
                 None if shard_clients == "group" else shard_clients)
                 if torch.distributed.is_available() and torch.distributed.is_initialized()
                 else 1)
-            kw = dict(expected_rows=-(-sample_count // world), borrow=True,
+            kw = dict(expected_rows=-(-sample_count // world), borrow=True, borrow_host=True,
                       mode=client_reduction)
             if shard_clients != "group":
                 kw["group"] = shard_clients
             aggregator_factory = partial(ClientShardedSerialAggregator, **kw)
         if aggregator_factory is None:
-            kw = dict(expected_rows=sample_count, borrow=True)
+            kw = dict(expected_rows=sample_count, borrow=True, borrow_host=True)
             if shard_over is None:
                 aggregator_factory = partial(SerialAggregator, **kw)
             else:

@@ -124,8 +124,10 @@ def _would_borrow(aggregator, t) -> bool:
     in place, or a host vector staged by the ingest worker while the next
     client trains (aggregators._Ingest.put_async)."""
     opts = getattr(aggregator, "_opts", None)
-    return (isinstance(aggregator, _DeviceSerialAggregator) and opts is not None
-            and opts.borrow and isinstance(t, torch.Tensor))
+    if not (isinstance(aggregator, _DeviceSerialAggregator) and opts is not None
+            and isinstance(t, torch.Tensor)):
+        return False
+    return opts.borrow if t.device.type == "cuda" else opts.borrow_host
 
 
 def pop_average(aggregator, key="local_params") -> torch.Tensor:

@@ -205,10 +205,10 @@ class _Like(object):
 
 class _Options(object):
     __slots__ = ("device", "slab_bytes", "max_rows", "flags", "expected_rows", "block_cols",
-                 "borrow", "fast")
+                 "borrow", "fast", "borrow_host")
 
     def __init__(self, device, slab_bytes, max_rows, flags, expected_rows, block_cols,
-                 borrow=False, fast=False):
+                 borrow=False, fast=False, borrow_host=False):
         self.device = device
         self.slab_bytes = slab_bytes
         self.max_rows = max_rows
@@ -217,6 +217,7 @@ class _Options(object):
         self.block_cols = block_cols
         self.borrow = borrow
         self.fast = fast
+        self.borrow_host = borrow_host
 
 
 class _TensorEntry(object):
@@ -251,6 +252,7 @@ class _DeviceEntry(_TensorEntry):
         # borrowed rows: HBM-resident client tensors reduced in place (no
         # snapshot copy); at most Bmax are held before they are drained
         self.borrow = opts.borrow
+        self.borrow_host = opts.borrow_host
         self.Bmax = max(1, min(opts.max_rows, budget // max(4, 4 * self.P)))
         self.borrowed: List = []
         self.borrowed_ptrs: List[int] = []  # their data pointers (the row table)
@@ -384,7 +386,7 @@ class _DeviceEntry(_TensorEntry):
             if src.device != self.dev:
                 src = src.to(self.dev)
             ops.pack_row(src.contiguous(), self.slab, r)  # D2D on the compute stream
-        elif self.borrow and src.is_contiguous():
+        elif self.borrow_host and src.is_contiguous():
             # handed over (serial_aggregation clones otherwise): copied while
             # the next client trains
             self.copy_event = self.agg._ingest(self.dev).put_async(
@@ -571,6 +573,12 @@ class SerialAggregator(object):
             reduction raise (torch's version counter is checked).  The round
             driver enables it, since its client messages are dropped right
             after ``receive_from_client``.
+        borrow_host: the same hand-over for host tensors: ``add`` returns
+            before the vector is copied into pinned staging; the ingest
+            worker copies and DMAs it while the caller goes on (the next
+            client trains).  Modifying it in place before that copy raises at
+            the reduction.  The round driver enables it; serial_aggregation
+            clones a vector whose ownership it cannot show.
         fast: for models too small for one column per lane to fill the chip
             (P below 65,536), split each column's K clients over several waves
             (FEDAGG_FAST).  Deterministic, but the summation order is no longer
@@ -582,11 +590,11 @@ class SerialAggregator(object):
                  max_rows: int = _DEFAULT_MAX_ROWS, flags: Optional[int] = None,
                  expected_rows: Optional[int] = None,
                  block_cols: Optional[int] = None, borrow: bool = False,
-                 fast: bool = False) -> None:
+                 fast: bool = False, borrow_host: bool = False) -> None:
         self._members: Dict = dict()
         self._reserved: Dict = dict()  # keys with reserved rows but no add yet
         self._opts = _Options(device, slab_bytes, max_rows, flags, expected_rows, block_cols,
-                              borrow, fast)
+                              borrow, fast, borrow_host)
     @staticmethod
     def _ingest(dev) -> _Ingest:
         return _ingest_for(dev)

@@ -406,7 +406,7 @@ def test_client_reusing_its_buffer_matches_reference(dev):
 
 
 def test_handed_over_host_rows_are_staged_after_add(dev):
-    """borrow=True with host vectors (the round driver's aggregator under
+    """borrow_host=True with host vectors (the round driver's aggregator under
     device="cpu"): each handed-over vector is copied into pinned staging and
     DMA'd by the ingest worker after add returns (while the next client
     trains), in arrival order, interleaved with HBM rows; the round is the
@@ -416,7 +416,7 @@ def test_handed_over_host_rows_are_staged_after_add(dev):
     K, P = 23, 199_210
     X = V.client_rows("realistic", K, P, 8)
     w = V.client_weights("fedavg", K, 8)
-    agg = SerialAggregator(borrow=True, max_rows=5)
+    agg = SerialAggregator(borrow=True, borrow_host=True, max_rows=5)
     for k in range(K):
         src = torch.from_numpy(X[k].copy())
         if k % 5 == 4:
@@ -438,7 +438,7 @@ def test_handed_over_host_row_mutated_in_place_raises(dev):
     from fedsim_amd.utils import SerialAggregator
     from fedsim_amd.utils.aggregators import _ingest_for
 
-    agg = SerialAggregator(borrow=True)
+    agg = SerialAggregator(borrow=True, borrow_host=True)
     gate = threading.Event()
     _ingest_for(dev).pool.submit(gate.wait)  # the worker is busy until released
     t = torch.ones(1 << 20)
@@ -459,7 +459,7 @@ def test_host_client_keeping_its_vector_is_cloned(dev):
     K, P = 6, 65_537
     X = V.client_rows("realistic", K, P, 9)
     w = V.client_weights("fedavg", K, 9)
-    agg = SerialAggregator(borrow=True)
+    agg = SerialAggregator(borrow=True, borrow_host=True)
     kept = []
     for k, msg in enumerate(V.client_messages(X, w)):
         kept.append(msg["local_params"])  # the client keeps its tensor
