@@ -231,7 +231,8 @@ def test_round_driver_shard_over_option():
                       criterion_def="CrossEntropyScore", device="cpu", **kw)
 
     f = make()._aggregator_factory
-    assert f.func is SerialAggregator and f.keywords == dict(expected_rows=5, borrow=True)
+    assert f.func is SerialAggregator and f.keywords == dict(expected_rows=5, borrow=True,
+                                                             borrow_host=True)
     f = make(shard_over=["cuda:0", "cuda:1"])._aggregator_factory
     assert f.func is ShardedSerialAggregator and f.keywords["devices"] == ["cuda:0", "cuda:1"]
     f = make(shard_over="group")._aggregator_factory
@@ -242,7 +243,7 @@ def test_round_driver_shard_over_option():
 
     f = make(shard_clients="group", client_reduction="allreduce")._aggregator_factory
     assert f.func is ClientShardedSerialAggregator and f.keywords["mode"] == "allreduce"
-    assert "group" not in f.keywords and f.keywords["borrow"]
+    assert "group" not in f.keywords and f.keywords["borrow"] and f.keywords["borrow_host"]
     with pytest.raises(ValueError):
         make(shard_clients="group", shard_over="group")
     with pytest.raises(ValueError):
