@@ -532,9 +532,14 @@ class CentralFLAlgorithm(object):
     # ---- public API (centralized_fl_algorithm.py:466-631) -----------------
     def train(self, rounds: int, num_score_report_point: Optional[int] = None,
               train_split_name="train") -> Optional[Dict[str, Optional[float]]]:
+        from ...utils.aggregators import release_borrowed
+
         default_split_name = self._train_split_name
         self._train_split_name = train_split_name
-        ans = self._train(rounds=rounds, num_score_report_point=num_score_report_point)
+        try:
+            ans = self._train(rounds=rounds, num_score_report_point=num_score_report_point)
+        finally:
+            release_borrowed()  # the last round's borrowed client tensors
         self._train_split_name = default_split_name
         return ans
 

@@ -177,9 +177,20 @@ def _keep_until(event, tensors) -> None:
     _prune_keepalive()
 
 
-def _prune_keepalive() -> None:
-    while _KEEPALIVE and _KEEPALIVE[0][0].query():
-        _KEEPALIVE.popleft()
+def _prune_keepalive(wait: bool = False) -> None:
+    """Drop the entries whose reduction has run (``wait``: all of them, once
+    they have run -- the round driver calls this when training returns, so
+    the last round's client tensors are not held after it)."""
+    while _KEEPALIVE and (wait or _KEEPALIVE[0][0].query()):
+        ev, _ = _KEEPALIVE.popleft()
+        if wait:
+            ev.synchronize()
+
+
+def release_borrowed() -> None:
+    """Wait for every reduction still reading borrowed client tensors and
+    release them."""
+    _prune_keepalive(wait=True)
 
 
 def _ingest_for(dev: torch.device) -> _Ingest:
