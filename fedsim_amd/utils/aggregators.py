@@ -31,7 +31,9 @@ from __future__ import annotations
 import os
 import struct
 from collections import deque
+import threading
 from concurrent.futures import Future, ThreadPoolExecutor
+from concurrent.futures import wait as _wait_futures
 from typing import Dict, List, Optional
 
 import torch
@@ -92,10 +94,11 @@ class _Ingest(object):
     after its previous copies have completed.  One ring per device is shared
     by all aggregators (the round driver makes a new one every round).
 
-    Every put runs on ONE worker thread (in submission order, so the slots
-    and the copy stream see one sequence).  ``put`` waits for it: the
-    snapshot is taken when add returns, as the reference's clone.
-    ``put_async`` does not: for a host vector the client handed over (the
+    The puts run one at a time in submission order (the slots and the copy
+    stream see one sequence).  ``put`` runs on the calling thread, after any
+    queued asynchronous put: the snapshot is taken when add returns, as the
+    reference's clone.  ``put_async`` runs on ONE worker thread and returns
+    at once: for a host vector the client handed over (the
     round driver's borrowing aggregator, training/utils.py ``_handed_over``),
     the pageable-to-pinned copy and the DMA then run while the next client
     trains instead of between the two clients (tools/bench_host_rounds.py:
@@ -112,13 +115,19 @@ class _Ingest(object):
         self.i = 0
         self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedsim-ingest",
                                        initializer=torch.cuda.set_device, initargs=(dev,))
+        self.lock = threading.Lock()
+        self.last: Optional[Future] = None  # the latest asynchronous put
 
     def put(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None):
-        return self.pool.submit(self._put, src, Xb, r, wait_event, None).result()
+        if self.last is not None:
+            _wait_futures([self.last])  # its error, if any, is its entry's to raise
+            self.last = None
+        return self._put(src, Xb, r, wait_event, None)
 
     def put_async(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None) -> Future:
         """Future of put's event; ``src`` must not change until it resolves."""
-        return self.pool.submit(self._put, src, Xb, r, wait_event, src._version)
+        self.last = self.pool.submit(self._put, src, Xb, r, wait_event, src._version)
+        return self.last
 
     @staticmethod
     def _slot(bufs, i, P, **kw):
@@ -129,6 +138,10 @@ class _Ingest(object):
         return buf[:P]
 
     def _put(self, src, Xb, r, wait_event, version):
+        with self.lock:
+            return self._put_locked(src, Xb, r, wait_event, version)
+
+    def _put_locked(self, src, Xb, r, wait_event, version):
         if version is not None and src._version != version:
             raise RuntimeError(
                 "a host client tensor was modified in place after SerialAggregator.add(); "
