@@ -835,9 +835,16 @@ class ClientShardedSerialAggregator(SerialAggregator):
         return self._ordered_sum(owners, local_partial, n)
 
     def broadcast_from(self, t: torch.Tensor, src: int) -> torch.Tensor:
-        """Collective: ``t`` on rank ``src`` copied into ``t`` on every rank."""
-        if not self._solo:
-            _broadcast(t, _global_rank(self._group, src), self._group)
+        """Collective: ``t`` on rank ``src`` copied into ``t`` on every rank
+        (a host tensor under RCCL travels through this rank's GPU)."""
+        if self._solo:
+            return t
+        if t.device.type == "cpu" and dist.get_backend(self._group) != dist.Backend.GLOO:
+            d = t.to(self._reduce_device())
+            _broadcast(d, _global_rank(self._group, src), self._group)
+            t.copy_(d)
+            return t
+        _broadcast(t, _global_rank(self._group, src), self._group)
         return t
 
     def _apply_step(self, step: ops.ServerStep, avg: torch.Tensor) -> None:
