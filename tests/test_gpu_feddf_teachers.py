@@ -435,6 +435,40 @@ def test_pad_lrn_maxpool_slide_vs_planes(case):
         assert float((np.abs(got - exp) / ulp).max()) <= 8.0
 
 
+@pytest.mark.parametrize("shape,lrn", [
+    ((3, 64, 24, 24), None),                          # SimpleCNN2 pool1 geometry, no LRN
+    ((3, 64, 24, 24), (4, 0.001 / 9, 0.75, 1.0)),     # pool1 as the model runs it
+    ((5, 64, 12, 12), (4, 0.001 / 9, 0.75, 1.0)),     # pool2
+    ((2, 37, 12, 12), None),                          # ragged last channel block
+])
+def test_pad_lrn_maxpool_signed_zeros_and_nans(shape, lrn):
+    """The 3 x 3 pool's maximum3 fast path falls back to the scan rule for
+    windows holding a -0 or a NaN: with many +-0 windows (first zero in
+    window order decides the sign) and NaNs sprinkled in, the sliding pass is
+    bit for bit the per-block pass (pool_planes' scan) and, without LRN, the C
+    oracle."""
+    from conftest import bits
+    from fedsim_amd import ops
+    from oracle import ref
+
+    g = torch.Generator(device=DEV).manual_seed(sum(shape) + (lrn is None))
+    x = torch.randn(*shape, device=DEV, generator=g)
+    x = torch.where(x < 0.3, torch.zeros_like(x), x)        # most windows all zero
+    sign = torch.rand(*shape, device=DEV, generator=g) < 0.5
+    x = torch.where(sign & (x == 0), -x, x)                 # -0 / +0 mixed
+    x.view(-1)[:: 1013] = float("nan")
+    pads, pool = (0, 1, 0, 1), (3, 3, 2, 2, 0, 0)
+    y = ops.pad_lrn_maxpool(x, pads, lrn, pool)
+    y_planes = ops.pad_lrn_maxpool(x, pads, lrn, pool, planes=True)
+    got = bits(y.cpu().numpy())
+    np.testing.assert_array_equal(got, bits(y_planes.cpu().numpy()))
+    assert (got == np.uint32(0x80000000)).any() and (got == 0).any()  # both zero signs out
+    assert np.isnan(y.cpu().numpy()).any()
+    if lrn is None:
+        exp = ref.pad_lrn_maxpool(x.cpu().numpy(), pads, lrn, pool)
+        np.testing.assert_array_equal(got, bits(exp))
+
+
 def test_pad_lrn_maxpool_special_values():
     """NaN propagates through the max pool and +-inf through pooling without
     LRN, as torch's max_pool2d does; 5-D input (teachers x images)."""

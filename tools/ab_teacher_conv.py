@@ -2,7 +2,8 @@
 at K stacked teachers, B = 64 samples, timed per launch with HIP events:
 conv1 (3 -> 64, 5x5, 24x24), the pad / LRN / max-pool pass after it, conv2
 (64 -> 64, 5x5, 12x12) and the pass after that (sliding channel window, and
-FEDAGG_POOL_PLANES: the per-block kernels, "_planes").  Several libfedagg BUILD
+FEDAGG_POOL_PLANES: the per-block kernels, "_planes"), and SimpleCNN's 2 x 2 /
+padding-1 pool on the same planes ("pool_cnn").  Several libfedagg BUILD
 variants can be given; each is its own ctypes handle, run interleaved in one
 process, and every output is compared bitwise with the first library's.
 The convolutions run both ways: the default kernel choice ("lds" for these
@@ -66,8 +67,11 @@ def main():
         ops.check(rc, "conv")
         return y
 
-    def pad_pool(lib, x, planes=False):
-        args = ops.pool_args(x.shape, (0, 1, 0, 1), lrn, pool, planes=planes)
+    def pad_pool(lib, x, planes=False, cnn=False):
+        # cnn: SimpleCNN's pool after conv2 (max_pool2d(2, 2, padding 1), no
+        # pad / LRN; simple_models.py:155-159), on the same 12 x 12 planes
+        args = (ops.pool_args(x.shape, (0, 0, 0, 0), None, (2, 2, 2, 2, 1, 1), planes=planes)
+                if cnn else ops.pool_args(x.shape, (0, 1, 0, 1), lrn, pool, planes=planes))
         oh, ow = ops.pool_output(args)
         y = torch.empty(*x.shape[:-2], oh, ow, device=dev)
         ops.check(lib.fedagg_pad_lrn_maxpool_f32(x.data_ptr(), ctypes.byref(args), y.data_ptr(),
@@ -91,9 +95,12 @@ def main():
         "pool2": (lambda lib: pad_pool(lib, c2), 0.0, 4.0 * K * M * 64 * (144 + 36)),
         "pool1_planes": (lambda lib: pad_pool(lib, c1, True), 0.0, 4.0 * K * M * 64 * (576 + 144)),
         "pool2_planes": (lambda lib: pad_pool(lib, c2, True), 0.0, 4.0 * K * M * 64 * (144 + 36)),
+        "pool_cnn": (lambda lib: pad_pool(lib, c2, cnn=True), 0.0, 4.0 * K * M * 64 * (144 + 49)),
+        "pool_cnn_planes": (lambda lib: pad_pool(lib, c2, True, cnn=True), 0.0,
+                            4.0 * K * M * 64 * (144 + 49)),
     }
     ref = {name: fn(libs[0]) for name, (fn, _, _) in layers.items()}
-    for name in ("pool1", "pool2"):  # sliding window vs per-block kernels: same bits
+    for name in ("pool1", "pool2", "pool_cnn"):  # sliding window vs per-block kernels: same bits
         same = torch.equal(ref[name].view(torch.int32), ref[name + "_planes"].view(torch.int32))
         print(json.dumps({"check": f"{name} slide vs planes", "bitwise": same}), flush=True)
         assert same
