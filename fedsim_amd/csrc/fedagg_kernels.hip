@@ -2601,6 +2601,74 @@ __device__ __forceinline__ void pool_planes_step(const float* plane, int cbn, in
   }
 }
 
+// A K x K pool (K = 2, 3: the reference CNNs' pools) of one block with the
+// window offsets mapped once per workgroup (src[i]: LDS index of the
+// top-left member of output e = t + 256 i, the same for every block of the
+// workgroup) over planes that carry the pool's padding as a -inf border (a
+// -inf member is what max_pool2d's skipped padding is to the scan), and the
+// max taken with v_maximum3_f32 (IEEE maximum: NaN-propagating, -0 < +0).
+// That equals the scan-order rule of pool_planes_step (a later element
+// replaces the running max when greater or NaN) unless the window holds a
+// NaN (which NaN's bits) or a -0 (which zero's sign): the lanes whose window
+// does -- the signed integer minimum of the members is INT_MIN exactly for a
+// -0, the maximum is NaN for a NaN -- redo the scan.  3 x 3: four maximum3 +
+// four min3_i32 per output instead of nine compare / NaN-test / select
+// triples and the per-output index multiplies and bounds.
+struct PoolStep {  // output e = t + 256 i of a block: its window, stepped
+  int src, oh, ow;  // for i = 0: LDS index of the top-left member, its row, column
+  int d_src, d_oh, d_ow;       // one step of 256 outputs in (channel, row, column) digits
+  int wrap_ow_src, wrap_oh_src;  // src correction when a column / row digit wraps
+  int OH, OW;
+};
+
+template <int K, int NI>
+__device__ __forceinline__ void pool_mapped(const float* plane, const PoolStep& ps, int pitch,
+                                            int total, float* __restrict__ yn) {
+  constexpr int KK = K * K;
+  int src = ps.src, oh = ps.oh, ow = ps.ow;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int e = static_cast<int>(threadIdx.x) + 256 * i;
+    if (i > 0) {
+      src += ps.d_src;
+      oh += ps.d_oh;
+      ow += ps.d_ow;
+      if (ow >= ps.OW) {
+        ow -= ps.OW;
+        ++oh;
+        src += ps.wrap_ow_src;
+      }
+      if (oh >= ps.OH) {
+        oh -= ps.OH;
+        src += ps.wrap_oh_src;
+      }
+    }
+    if (e < total) {
+      const float* p = plane + src;
+      float v[KK];
+#pragma unroll
+      for (int h = 0; h < K; ++h)
+#pragma unroll
+        for (int w = 0; w < K; ++w) v[K * h + w] = p[h * pitch + w];
+      float m = v[0];
+      int mn = __builtin_bit_cast(int, v[0]);
+#pragma unroll
+      for (int t = 1; t < KK; ++t) {
+        m = __builtin_elementwise_maximum(m, v[t]);
+        mn = min(mn, __builtin_bit_cast(int, v[t]));
+      }
+      float r = m;
+      if (mn == INT_MIN || m != m) {  // a -0 or a NaN in the window: the scan
+        r = -__builtin_inff();
+#pragma unroll
+        for (int t = 0; t < KK; ++t)
+          if (v[t] > r || __builtin_isnan(v[t])) r = v[t];
+      }
+      yn[e] = r;
+    }
+  }
+}
+
 // SIZE = the LRN window (0: no LRN) known at compile time: each thread loads
 // the whole channel window of its pixel for the block (CB + SIZE - 1 values,
 // all loads in flight at once) and normalises CB channels from registers.
@@ -2818,6 +2886,47 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
             static_cast<unsigned>(iw) < static_cast<unsigned>(W);
     voff[i] = in[i] ? static_cast<uint32_t>(ih * W + iw) * 4u : kOut;
   }
+  // 2 x 2 and 3 x 3 pools whose block fits NM outputs per thread (the
+  // reference CNNs' pools: stride 2, a quarter of the plane's positions per
+  // channel) take pool_mapped: the planes in LDS get the pool's padding as a
+  // -inf border (pitch WpE, HpWpE per channel) and this thread's window
+  // offsets are mapped once.  Other pools: pool_planes_step, no border.
+  constexpr int NM = (CB * NQ + 3) / 4;
+  const int pk = static_cast<int>(a.pool_kh);
+  const bool map = a.pool_kh == a.pool_kw && (pk == 2 || pk == 3) && CB * OHW <= 256 * NM;
+  const int bph = map ? static_cast<int>(a.pool_ph) : 0, bpw = map ? static_cast<int>(a.pool_pw) : 0;
+  const int WpE = Wp + 2 * bpw;
+  const int HpWpE = (Hp + 2 * bph) * WpE;
+  PoolStep ps;
+  {
+    const int sh = static_cast<int>(a.pool_sh), sw = static_cast<int>(a.pool_sw);
+    const int ow_n = static_cast<int>(OW), oh_n = static_cast<int>(OH);
+    const int e = threadIdx.x;
+    const int cc = e / OHW;
+    ps.oh = (e - cc * OHW) / ow_n;
+    ps.ow = e - cc * OHW - ps.oh * ow_n;
+    ps.src = cc * HpWpE + ps.oh * sh * WpE + ps.ow * sw;
+    const int dcc = 256 / OHW;
+    ps.d_oh = (256 - dcc * OHW) / ow_n;
+    ps.d_ow = 256 - dcc * OHW - ps.d_oh * ow_n;
+    ps.d_src = dcc * HpWpE + ps.d_oh * sh * WpE + ps.d_ow * sw;
+    ps.wrap_ow_src = sh * WpE - ow_n * sw;
+    ps.wrap_oh_src = HpWpE - oh_n * sh * WpE;
+    ps.OH = oh_n;
+    ps.OW = ow_n;
+  }
+  // LDS index of each of this thread's plane positions inside the border
+  int wq[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    const int ph = q / Wp;
+    wq[i] = (ph + bph) * WpE + (q - ph * Wp) + bpw;
+  }
+  if (bph | bpw) {  // the border, once: the blocks write inside it only
+    for (int e = threadIdx.x; e < CB * HpWpE; e += 256) plane[e] = -__builtin_inff();
+    __syncthreads();
+  }
   // channel ch of every position of this thread (0 outside [0, C): the
   // LRN's zero channels; padded positions read past the descriptor: 0)
   auto load = [&](float (&dst)[NQ], int ch) {
@@ -2828,13 +2937,21 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
                                                   xres, static_cast<int>(voff[i]), ch * HW * 4, 0))
                   : 0.f;
   };
-  float win[SW][NQ];  // win[t] = channel c - LO + t of the current channel c
-  float sq[SW][NQ];   // its squares, each computed once
+  // The window of the current channel c: channel c - LO + t (t < SW) and its
+  // square (each computed once).  RING (CB a multiple of SW, SimpleCNN2's
+  // size-4 LRN): a ring whose slot for step j of a block is (j + t) % SW, a
+  // compile-time index in the unrolled block, so nothing moves; else the
+  // registers shift down one slot per channel.
+  constexpr bool RING = CB % SW == 0;
+  auto slot = [](int j, int t) { return RING ? (j + t) % SW : t; };
+  float win[SW][NQ];
+  float sq[SW][NQ];
 #pragma unroll
   for (int t = 0; t + 1 < SW; ++t) {
-    load(win[t + 1], g0 - LO + t);  // shifted in before use
+    const int u = RING ? t : t + 1;  // the shifting form shifts them in before use
+    load(win[u], g0 - LO + t);
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) sq[t + 1][i] = win[t + 1][i] * win[t + 1][i];
+    for (int i = 0; i < NQ; ++i) sq[u][i] = win[u][i] * win[u][i];
   }
   float raw[CB][NQ];  // the lead channels c + LEAD of the block in flight
 #pragma unroll
@@ -2846,17 +2963,19 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 #pragma unroll
     for (int j = 0; j < CB; ++j) {
       if (j < cbn) {
+        if constexpr (!RING) {
 #pragma unroll
-        for (int t = 0; t + 1 < SW; ++t)
+          for (int t = 0; t + 1 < SW; ++t)
 #pragma unroll
-          for (int i = 0; i < NQ; ++i) {
-            win[t][i] = win[t + 1][i];
-            sq[t][i] = sq[t + 1][i];
-          }
+            for (int i = 0; i < NQ; ++i) {
+              win[t][i] = win[t + 1][i];
+              sq[t][i] = sq[t + 1][i];
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
-          win[SW - 1][i] = raw[j][i];
-          sq[SW - 1][i] = raw[j][i] * raw[j][i];
+          win[slot(j, SW - 1)][i] = raw[j][i];
+          sq[slot(j, SW - 1)][i] = raw[j][i] * raw[j][i];
         }
         // lrn_value<SIZE, true> of every position without a per-lane branch:
         // the fast v * r everywhere, the powf division only when some lane
@@ -2866,13 +2985,13 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
         bool slow = false;
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
-          vv[i] = win[LO][i];
+          vv[i] = win[slot(j, LO)][i];
           if constexpr (SIZE > 0) {
             // ATen's sum from +0 in channel order: a square is never -0,
             // so +0 + sq[0] is sq[0] and the chain starts there
-            float sum = sq[0][i];
+            float sum = sq[slot(j, 0)][i];
 #pragma unroll
-            for (int t = 1; t < SIZE; ++t) sum = sum + sq[t][i];
+            for (int t = 1; t < SIZE; ++t) sum = sum + sq[slot(j, t)][i];
             bb[i] = lrn_base<SIZE>(sum, size_f, a.lrn_alpha, a.lrn_k);
             float r;
             const bool fast = lrn_fast_scale(bb[i], nbeta, r);
@@ -2886,7 +3005,7 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
             for (int i = 0; i < NQ; ++i) {
               float r;
               if (in[i] && !lrn_fast_scale(bb[i], nbeta, r))
-                vv[i] = win[LO][i] / lrn_powf(bb[i], a.lrn_beta);
+                vv[i] = win[slot(j, LO)][i] / lrn_powf(bb[i], a.lrn_beta);
             }
           }
         }
@@ -2894,7 +3013,7 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
         for (int i = 0; i < NQ; ++i) {
           // positions 256 i + t of the first NQ - 1 groups are all inside
           if (i + 1 < NQ || static_cast<int>(threadIdx.x) + 256 * i < HpWp)
-            plane[j * HpWp + threadIdx.x + 256 * i] = vv[i];
+            plane[j * HpWpE + wq[i]] = vv[i];
         }
       }
     }
@@ -2904,8 +3023,13 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
       for (int j = 0; j < CB; ++j) load(raw[j], c0 + CB + LEAD + j);
     }
     __syncthreads();
-    pool_planes_step(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
-                     y + (n * a.C + c0) * OHW);
+    if (map && pk == 3)
+      pool_mapped<3, NM>(plane, ps, WpE, cbn * OHW, y + (n * a.C + c0) * OHW);
+    else if (map)
+      pool_mapped<2, NM>(plane, ps, WpE, cbn * OHW, y + (n * a.C + c0) * OHW);
+    else
+      pool_planes_step(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
+                       y + (n * a.C + c0) * OHW);
     __syncthreads();
   }
 }
@@ -3331,7 +3455,9 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
     if (G < 1) G = 1;
     const int64_t CG = ((nb + G - 1) / G) * cbs;
     G = (a.C + CG - 1) / CG;
-    const size_t slds = static_cast<size_t>(cbs * Hp * Wp) * sizeof(float);
+    // planes with the pool padding as a border (k_pad_lrn_maxpool_slide)
+    const size_t slds = static_cast<size_t>(cbs * (Hp + 2 * a.pool_ph) * (Wp + 2 * a.pool_pw)) *
+                        sizeof(float);
     for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {
       const dim3 g(static_cast<unsigned>(G),
                    static_cast<unsigned>(a.N - n0 < 65535 ? a.N - n0 : 65535));

@@ -435,18 +435,25 @@ def test_pad_lrn_maxpool_slide_vs_planes(case):
         assert float((np.abs(got - exp) / ulp).max()) <= 8.0
 
 
-@pytest.mark.parametrize("shape,lrn", [
-    ((3, 64, 24, 24), None),                          # SimpleCNN2 pool1 geometry, no LRN
-    ((3, 64, 24, 24), (4, 0.001 / 9, 0.75, 1.0)),     # pool1 as the model runs it
-    ((5, 64, 12, 12), (4, 0.001 / 9, 0.75, 1.0)),     # pool2
-    ((2, 37, 12, 12), None),                          # ragged last channel block
+P3 = ((0, 1, 0, 1), (3, 3, 2, 2, 0, 0))   # SimpleCNN2's pad + 3 x 3 / 2 pool
+P2 = ((0, 0, 0, 0), (2, 2, 2, 2, 1, 1))   # SimpleCNN's 2 x 2 / 2 pool, padding 1
+
+
+@pytest.mark.parametrize("shape,lrn,geom", [
+    ((3, 64, 24, 24), None, P3),                          # SimpleCNN2 pool1 geometry, no LRN
+    ((3, 64, 24, 24), (4, 0.001 / 9, 0.75, 1.0), P3),     # pool1 as the model runs it
+    ((5, 64, 12, 12), (4, 0.001 / 9, 0.75, 1.0), P3),     # pool2
+    ((2, 37, 12, 12), None, P3),                          # ragged last channel block
+    ((4, 64, 12, 12), None, P2),                          # SimpleCNN pool2: -inf border
+    ((3, 32, 26, 26), None, P2),                          # SimpleCNN pool1 shape, 4 x 256 planes
+    ((2, 21, 9, 11), (3, 0.01, 0.5, 2.0), ((1, 0, 2, 1), (3, 3, 2, 2, 1, 1))),  # both paddings
 ])
-def test_pad_lrn_maxpool_signed_zeros_and_nans(shape, lrn):
-    """The 3 x 3 pool's maximum3 fast path falls back to the scan rule for
-    windows holding a -0 or a NaN: with many +-0 windows (first zero in
-    window order decides the sign) and NaNs sprinkled in, the sliding pass is
-    bit for bit the per-block pass (pool_planes' scan) and, without LRN, the C
-    oracle."""
+def test_pad_lrn_maxpool_signed_zeros_and_nans(shape, lrn, geom):
+    """The mapped 2 x 2 / 3 x 3 pools' maximum3 fast path falls back to the
+    scan rule for windows holding a -0 or a NaN, and the pool padding is a
+    -inf border: with many +-0 windows (first zero in window order decides
+    the sign) and NaNs sprinkled in, the sliding pass is bit for bit the
+    per-block pass (pool_planes' scan) and, without LRN, the C oracle."""
     from conftest import bits
     from fedsim_amd import ops
     from oracle import ref
@@ -457,7 +464,7 @@ def test_pad_lrn_maxpool_signed_zeros_and_nans(shape, lrn):
     sign = torch.rand(*shape, device=DEV, generator=g) < 0.5
     x = torch.where(sign & (x == 0), -x, x)                 # -0 / +0 mixed
     x.view(-1)[:: 1013] = float("nan")
-    pads, pool = (0, 1, 0, 1), (3, 3, 2, 2, 0, 0)
+    pads, pool = geom
     y = ops.pad_lrn_maxpool(x, pads, lrn, pool)
     y_planes = ops.pad_lrn_maxpool(x, pads, lrn, pool, planes=True)
     got = bits(y.cpu().numpy())
