@@ -28,6 +28,7 @@ fallback for them — without a HIP device / libfedagg the add raises.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import struct
 from collections import deque
@@ -157,7 +158,13 @@ class _Ingest(object):
             host = src  # DMA straight from the caller's pinned buffer
         else:
             host = self._slot(self.hbufs, i, P, pin_memory=True)
-            host.copy_(src)
+            if version is not None and src.dtype == torch.float32 and src.is_contiguous():
+                # on the worker thread, while the next client trains: one
+                # single-threaded memcpy (torch's copy_ would start its own
+                # OpenMP team and contend with the training threads)
+                ctypes.memmove(host.data_ptr(), src.data_ptr(), 4 * P)
+            else:
+                host.copy_(src)
         with torch.cuda.stream(self.stream):
             dslot.copy_(host, non_blocking=True)
         if wait_event is not None:
@@ -198,6 +205,21 @@ def _prune_keepalive(wait: bool = False) -> None:
         ev, _ = _KEEPALIVE.popleft()
         if wait:
             ev.synchronize()
+
+
+_PRUNE_EVERY = 32  # adds between two completion queries while entries are pending
+_prune_tick = 0
+
+
+def _prune_keepalive_at_add() -> None:
+    """The prune an ``add`` runs: one event query per _PRUNE_EVERY adds (the
+    last round's reduction may still be running through the first adds of
+    the next round; a query per add is ≈1 µs of host time per client)."""
+    global _prune_tick
+    _prune_tick += 1
+    if _prune_tick >= _PRUNE_EVERY:
+        _prune_tick = 0
+        _prune_keepalive()
 
 
 def release_borrowed() -> None:
@@ -362,7 +384,7 @@ class _DeviceEntry(_TensorEntry):
     # -- reference semantics -------------------------------------------------
     def add(self, value: torch.Tensor, weight) -> None:
         if _KEEPALIVE:  # an earlier round's borrowed rows, once it has run
-            _prune_keepalive()
+            _prune_keepalive_at_add()
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
         if value.shape != self.shape:
             raise ValueError(

@@ -27,7 +27,7 @@ crop), 1000 clients x 50 samples, K = 10; fed-learn defaults otherwise
 (epochs 5, batch 32, local SGD lr 0.1 wd 1e-3, server SGD lr 1.0;
 fedsim_cli/fed_learn.py:58-161).
 
-python tools/bench_host_rounds.py [--config 1|2] [--rounds 3]
+python tools/bench_host_rounds.py [--config 1|2] [--rounds 3] [--reps 2] [--legs gpu,ref]
 """
 import argparse
 import json
@@ -96,6 +96,10 @@ def main():
     ap.add_argument("--config", type=int, default=1, choices=[1, 2])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--legs", default="gpu,ref",
+                    help="comma- or plus-separated: gpu (the round driver's aggregator: host vectors staged on the ingest "
+                         "worker thread), gpu_sync (staged on the calling thread at add), ref")
     a = ap.parse_args()
     if a.threads:
         torch.set_num_threads(a.threads)
@@ -123,10 +127,16 @@ def main():
                     sched.step()
             return serial_aggregator.pop_all()
 
-    legs = {"gpu": (FedAvg, None), "ref": (RefFedAvg, ReferenceSerialAggregator)}
+    from fedsim_amd.utils import SerialAggregator
+
+    K = int(0.01 * cfg["clients"])
+    legs = {"gpu": (FedAvg, None), "ref": (RefFedAvg, ReferenceSerialAggregator),
+            "gpu_sync": (FedAvg, partial(SerialAggregator, expected_rows=K, borrow=True,
+                                         borrow_host=False))}
     out = []
-    for rep in range(2):
-        for leg, (base, agg) in legs.items():
+    for rep in range(a.reps):
+        for leg in a.legs.replace("+", ",").split(","):
+            base, agg = legs[leg]
             clock = {}
             random.seed(7)
             torch.manual_seed(7)
@@ -144,7 +154,6 @@ def main():
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
             wall = time.perf_counter() - t0
-            K = int(0.01 * cfg["clients"])
             cloud = alg.get_server_storage().read("cloud_params").detach()
             rec = dict(config=a.config, leg=leg, rep=rep, model=cfg["model"], K=K,
                        rounds=a.rounds, threads=torch.get_num_threads(),
