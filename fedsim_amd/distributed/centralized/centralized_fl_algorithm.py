@@ -425,7 +425,9 @@ class CentralFLAlgorithm(object):
             contexts.update(e["ctx"])
         diverged_at = None
         for p in range(len(clients)):
-            if p > 0 and self._check_client_context:
+            # a message without plain-data entries (FedAvg's: the model) has
+            # nothing to compare, and send_to_client is not called twice
+            if p > 0 and self._check_client_context and contexts.get(p):
                 now = _context_fingerprint(self._send_to_client(clients[p]))
                 if now != contexts.get(p):
                     keys = sorted(k for k in set(now or {}) | set(contexts.get(p) or {})
