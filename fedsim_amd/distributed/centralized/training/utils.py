@@ -205,14 +205,17 @@ def fused_server_step(algo: str, cloud: torch.Tensor, avg, optimizer,
             avg, source = agg.pop(key), None
     if source is None:
         dev = _hip_device_for(avg, cloud)
+    state = optimizer.state[cloud]
+    prev = state.get("momentum_buffer") if cfg["momentum"] != 0 else None
+    if _host_state(cloud, aux, prev, dev):
+        return _fused_server_step_host(algo, cloud, avg, source, optimizer, cfg, coef, aux,
+                                       want_avg_prev, dev, prev)
     c = cloud.data if cloud.device == dev else cloud.data.to(dev)
     x = _work_copy(aux, dev) if aux is not None else None
     ap = torch.empty_like(c) if want_avg_prev else None
     g = torch.empty_like(c)
-    state = optimizer.state[cloud]
     buf, init = None, False
     if cfg["momentum"] != 0:
-        prev = state.get("momentum_buffer")
         init = prev is None
         buf = torch.empty_like(c) if init else _work_copy(prev, dev)
     step = ops.ServerStep(algo, c.view(-1), lr=cfg["lr"], momentum=cfg["momentum"],
@@ -234,6 +237,73 @@ def fused_server_step(algo: str, cloud: torch.Tensor, avg, optimizer,
     optimizer._opt_called = True
     x_out = None if x is None else x.view_as(aux).to(aux.device)
     ap_out = None if ap is None else ap.view_as(cloud).to(cloud.device)
+    return x_out, ap_out
+
+
+def _host_state(cloud, aux, prev, dev) -> bool:
+    """The cloud (and the aux vector and momentum buffer, when present) in
+    host memory, fp32, while the step runs on the GPU: FedSim's device="cpu"
+    runs (BASELINE config 1)."""
+    if dev.type != "cuda" or cloud.device.type != "cpu":
+        return False
+    return all(t is None or (t.device.type == "cpu" and t.dtype == torch.float32)
+               for t in (aux, prev))
+
+
+def _fused_server_step_host(algo, cloud, avg, source, optimizer, cfg, coef, aux, want_avg_prev,
+                            dev, prev):
+    """fused_server_step for host-resident server state: the state crosses
+    PCIe as ONE pinned DMA each way instead of one pageable copy per tensor
+    (H2D of the cloud, D2H of the cloud and of its grad, plus the momentum
+    buffer / aux / previous average when the algorithm has them).  One device
+    buffer holds every vector the kernel reads or writes; the results come
+    back into one pinned buffer whose rows become ``cloud.grad``, the
+    momentum buffer and the returned vectors (fresh tensors each round, as
+    the reference's step leaves them).  Same kernel, same bits."""
+    P = cloud.numel()
+    rows = ["c", "g"] + (["x"] if aux is not None else []) + \
+        (["ap"] if want_avg_prev else []) + (["buf"] if cfg["momentum"] != 0 else [])
+    at = {name: i for i, name in enumerate(rows)}
+    D = torch.empty(len(rows), P, dtype=torch.float32, device=dev)
+    ins = [("c", cloud.data)] + ([("x", aux)] if aux is not None else []) + \
+        ([("buf", prev)] if prev is not None else [])
+    hin = torch.empty(len(ins), P, dtype=torch.float32, pin_memory=True)
+    for j, (name, t) in enumerate(ins):
+        hin[j].copy_(t.detach().reshape(-1))
+    cur = torch.cuda.current_stream(dev)
+    if [at[name] for name, _ in ins] == list(range(len(ins))):
+        D[:len(ins)].copy_(hin, non_blocking=True)  # one DMA (inputs are the leading rows)
+    else:
+        for j, (name, _) in enumerate(ins):
+            D[at[name]].copy_(hin[j], non_blocking=True)
+    row = {name: D[i] for i, name in enumerate(rows)}
+    step = ops.ServerStep(algo, row["c"], lr=cfg["lr"], momentum=cfg["momentum"],
+                          dampening=cfg["dampening"], weight_decay=cfg["weight_decay"],
+                          nesterov=cfg["nesterov"], maximize=cfg["maximize"], coef=coef,
+                          aux=row.get("x"), avg_prev=row.get("ap"), momentum_buf=row.get("buf"),
+                          momentum_init=cfg["momentum"] != 0 and prev is None,
+                          grad_out=row["g"])
+    if source is not None:
+        agg, key = source
+        agg.pop_step(key, step)
+    else:
+        step.apply((avg if avg.device == dev else avg.to(dev)).reshape(-1).contiguous())
+    hout = torch.empty(len(rows), P, dtype=torch.float32, pin_memory=True)
+    hout.copy_(D, non_blocking=True)
+    done = torch.cuda.Event()
+    done.record(cur)
+    done.synchronize()
+    out = {name: hout[i] for i, name in enumerate(rows)}
+    cloud.data.copy_(out["c"].view_as(cloud))
+    optimizer.zero_grad()
+    cloud.grad = out["g"].view_as(cloud)
+    if "buf" in out:
+        optimizer.state[cloud]["momentum_buffer"] = out["buf"].view_as(cloud)
+    # The kernel replaced optimizer.step(); LR schedulers check this flag
+    # (torch/optim/lr_scheduler.py) to detect a step.
+    optimizer._opt_called = True
+    x_out = out["x"].view_as(aux) if aux is not None else None
+    ap_out = out["ap"].view_as(cloud) if want_avg_prev else None
     return x_out, ap_out
 
 
