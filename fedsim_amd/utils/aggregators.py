@@ -182,6 +182,14 @@ class _Ingest(object):
 
 _INGESTS: Dict = {}
 
+# Handed-over host vectors from this many floats (2 MB) on are staged by the
+# ingest worker; smaller ones on the calling thread at add.  With the clients'
+# training in the loop (tools/bench_host_rounds.py, profiles/r04i, r04k) the
+# worker saves 2.5-3 ms per round at config 2 (4.3 MB vectors: receive 1.0-1.7
+# vs 3.5-4.7 ms), while at config 1 (0.8 MB) its hand-off costs more at
+# optimize than the copies it moves (receive + optimize 1.1-1.4 vs 1.0-1.2 ms).
+_ASYNC_STAGE_MIN = 1 << 19
+
 
 # Borrowed client tensors after the reduction that read them was enqueued:
 # kept alive until its completion event, so their memory cannot be reused by
@@ -432,7 +440,7 @@ class _DeviceEntry(_TensorEntry):
             if src.device != self.dev:
                 src = src.to(self.dev)
             ops.pack_row(src.contiguous(), self.slab, r)  # D2D on the compute stream
-        elif self.borrow_host and src.is_contiguous():
+        elif self.borrow_host and src.is_contiguous() and src.numel() >= _ASYNC_STAGE_MIN:
             # handed over (serial_aggregation clones otherwise): copied while
             # the next client trains
             self.copy_event = self.agg._ingest(self.dev).put_async(

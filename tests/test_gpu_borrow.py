@@ -413,7 +413,7 @@ def test_handed_over_host_rows_are_staged_after_add(dev):
     oracle's bit for bit."""
     from fedsim_amd.utils import SerialAggregator
 
-    K, P = 23, 199_210
+    K, P = 23, 600_001  # above _ASYNC_STAGE_MIN: the worker stages them
     X = V.client_rows("realistic", K, P, 8)
     w = V.client_weights("fedavg", K, 8)
     agg = SerialAggregator(borrow=True, borrow_host=True, max_rows=5)
@@ -426,6 +426,24 @@ def test_handed_over_host_rows_are_staged_after_add(dev):
     out = agg.pop("p")
     assert out.device.type == "cpu"
     np.testing.assert_array_equal(bits(out.numpy()), bits(ref.reduce(X, w, W=sum(w))))
+
+
+def test_small_handed_over_host_rows_are_staged_at_add(dev):
+    """Below _ASYNC_STAGE_MIN a handed-over host vector is staged on the
+    calling thread at add (no worker hand-off), mixed with worker-staged
+    large ones of another key; both rounds are the oracle's bit for bit."""
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _ASYNC_STAGE_MIN
+
+    K, Ps, Pl = 9, 199_210, _ASYNC_STAGE_MIN + 3
+    Xs, Xl = V.client_rows("realistic", K, Ps, 10), V.client_rows("realistic", K, Pl, 11)
+    w = V.client_weights("fedavg", K, 10)
+    agg = SerialAggregator(borrow=True, borrow_host=True, max_rows=4)
+    for k in range(K):
+        agg.add("s", torch.from_numpy(Xs[k].copy()), w[k])
+        agg.add("l", torch.from_numpy(Xl[k].copy()), w[k])
+    np.testing.assert_array_equal(bits(agg.pop("s").numpy()), bits(ref.reduce(Xs, w, W=sum(w))))
+    np.testing.assert_array_equal(bits(agg.pop("l").numpy()), bits(ref.reduce(Xl, w, W=sum(w))))
 
 
 def test_handed_over_host_row_mutated_in_place_raises(dev):

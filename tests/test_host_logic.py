@@ -400,3 +400,29 @@ def test_changed_client_storage_keys():
     st.write("last_round", 3)
     st.write("new", 5)
     assert sorted(_changed_keys(st, state)) == ["d", "h", "last_round", "new"]
+
+
+def test_host_state_step_selection():
+    """fused_server_step takes the one-DMA-each-way host path exactly when
+    the cloud (and the aux vector / momentum buffer it has) live in host
+    memory as fp32 and the step runs on a HIP device; the device decision
+    only (nothing is allocated)."""
+    from fedsim_amd.distributed.centralized.training.utils import _host_state
+
+    hip = torch.device("cuda", 0)
+    cloud = torch.zeros(8)
+    assert _host_state(cloud, None, None, hip)
+    assert _host_state(cloud, torch.zeros(8), torch.zeros(8), hip)
+    assert not _host_state(cloud, torch.zeros(8, dtype=torch.float64), None, hip)
+    assert not _host_state(cloud, None, torch.zeros(8, device="meta"), hip)
+    assert not _host_state(torch.zeros(8, device="meta"), None, None, hip)
+    assert not _host_state(cloud, None, None, torch.device("cpu"))
+
+
+def test_async_host_staging_threshold():
+    """Handed-over host vectors are staged by the ingest worker from 2 MB on
+    (tools/bench_host_rounds.py: config 2's 4.3 MB vectors gain, config 1's
+    0.8 MB ones lose the hand-off)."""
+    from fedsim_amd.utils.aggregators import _ASYNC_STAGE_MIN
+
+    assert 199_210 < _ASYNC_STAGE_MIN <= 1_085_668
