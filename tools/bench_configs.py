@@ -116,7 +116,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     rng = np.random.default_rng(11)
     out = {}
-    only = set(a.only.split(","))
+    only = set(a.only.replace("+", ",").split(","))
 
     def report(name, K, P, t, extra=None):
         bytes_ = 4.0 * K * P * world
