@@ -1848,12 +1848,10 @@ __global__ __launch_bounds__(256) void k_teacher_conv2d(
 constexpr int kTC_XPK_LDS = 14;  // LDS float index bits of a packed staging offset
 constexpr int kTC_XPK_GLB = 18;  // global float offset bits
 
-// 3 waves per SIMD (4 spill 57 VGPRs: SimpleCNN2 conv2 7.50 vs 6.92 ms,
-// profiles/r02xi)
 template <int KS, int CC, int XM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_lds(
+__device__ __forceinline__ void conv2d_lds_tile(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
-    int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, const fedagg_conv2d_shape& s, int nslot,
     float* __restrict__ y, int relu) {
   constexpr int TAPS = KS * KS;
   constexpr int RC = TAPS * CC;  // reductions per chunk
@@ -2033,6 +2031,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       }
     }
   }
+}
+
+// Compiled for 3 waves per SIMD (4 spill 57 VGPRs: SimpleCNN2 conv2 7.50 vs
+// 6.92 ms, profiles/r02xi) ...
+template <int KS, int CC, int XM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_teacher_conv2d_lds(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
+    float* __restrict__ y, int relu) {
+  conv2d_lds_tile<KS, CC, XM>(x, x_kstride, params, params_kstride, w_off, b_off, s, nslot, y, relu);
+}
+
+// ... except chunks of 2 channels with 8 staging registers, which fit 4 waves
+// per SIMD in 128 VGPRs (16 B of scratch): SimpleCNN's conv2 3.632 -> 3.535 ms
+// per 500 teachers, same bits (profiles/r04s/; XM = 16 would spill 100 B)
+template <int KS, int CC, int XM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_teacher_conv2d_lds4(
+    const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
+    int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
+    float* __restrict__ y, int relu) {
+  conv2d_lds_tile<KS, CC, XM>(x, x_kstride, params, params_kstride, w_off, b_off, s, nslot, y, relu);
 }
 
 // ---------------------------------------------------------------------------
@@ -3312,6 +3331,9 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
 #define FEDAGG_CONV_LDS(KS, CC, XM)                                                          \
   hipLaunchKernelGGL((k_teacher_conv2d_lds<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
                      x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
+#define FEDAGG_CONV_LDS4(KS, CC, XM)                                                          \
+  hipLaunchKernelGGL((k_teacher_conv2d_lds4<KS, CC, XM>), grid, dim3(256), plan.lds, st, xk, \
+                     x_kstride, pk, params_kstride, w_off, b_off, s, plan.nslot, yk, relu)
 #define FEDAGG_CONV_FLAT(KS, CI, XM)                                                          \
   do {                                                                                        \
     if (ppad >= 0) {                                                                          \
@@ -3350,7 +3372,7 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
           else if (plan.xm == 12) FEDAGG_CONV_LDS(5, 4, 12);
           else FEDAGG_CONV_LDS(5, 4, 16);
         } else {
-          if (plan.xm == 8) FEDAGG_CONV_LDS(5, 2, 8); else FEDAGG_CONV_LDS(5, 2, 16);
+          if (plan.xm == 8) FEDAGG_CONV_LDS4(5, 2, 8); else FEDAGG_CONV_LDS(5, 2, 16);
         }
       } else {
         if (plan.cc == 4) {
@@ -3358,11 +3380,12 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
           else if (plan.xm == 12) FEDAGG_CONV_LDS(3, 4, 12);
           else FEDAGG_CONV_LDS(3, 4, 16);
         } else {
-          if (plan.xm == 8) FEDAGG_CONV_LDS(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
+          if (plan.xm == 8) FEDAGG_CONV_LDS4(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
         }
       }
 #undef FEDAGG_CONV_FLAT
 #undef FEDAGG_CONV_FLAT_H
+#undef FEDAGG_CONV_LDS4
 #undef FEDAGG_CONV_LDS
       const int rc = static_cast<int>(hipGetLastError());
       if (rc) return rc;
