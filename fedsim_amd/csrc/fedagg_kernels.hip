@@ -2438,11 +2438,12 @@ bool conv_lds_plan(const fedagg_conv2d_shape& s, ConvLdsPlan* p, int pool_pad = 
     }
   }
   if (pool_pad >= 0) return false;  // the pool is fused by the flat kernel only
-  // chunks of 2 channels where 4 would need 16 staging registers (SimpleCNN
-  // conv2, 32 ch at 14x14: whole teacher batch at K=1000 14.55 -> 13.97 ms,
-  // profiles/r02xa)
-  int cc = s.C >= 4 ? 4 : 2;
-  if (cc == 4 && cc * nslot * HW > 8 * 256) cc = 2;
+  // chunks of 2 channels: with 8 staging registers the kernel runs at 4
+  // waves per SIMD (k_teacher_conv2d_lds4), which beats chunks of 4 at 3
+  // (SimpleCNN2 conv2 6.973 -> 6.856 ms, SimpleCNN conv2 3.632 -> 3.535 ms
+  // per 500 teachers, profiles/r04s, r04u; at 3 waves chunks of 4 had led
+  // where they fit 8 registers, and 2 where 4 needed 16: profiles/r02xa)
+  const int cc = 2;
   const int64_t xtot = cc * nslot * HW;
   const int xm = xtot <= 8 * 256 ? 8 : 16;
   if (xtot > xm * 256) return false;
@@ -3366,22 +3367,10 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
             if (plan.xm == 8) FEDAGG_CONV_FLAT(3, 1, 8); else FEDAGG_CONV_FLAT(3, 1, 16);
           }
         }
-      } else if (plan.ks == 5) {
-        if (plan.cc == 4) {
-          if (plan.xm == 8) FEDAGG_CONV_LDS(5, 4, 8);
-          else if (plan.xm == 12) FEDAGG_CONV_LDS(5, 4, 12);
-          else FEDAGG_CONV_LDS(5, 4, 16);
-        } else {
-          if (plan.xm == 8) FEDAGG_CONV_LDS4(5, 2, 8); else FEDAGG_CONV_LDS(5, 2, 16);
-        }
+      } else if (plan.ks == 5) {  // chunks of 2 channels (conv_lds_plan)
+        if (plan.xm == 8) FEDAGG_CONV_LDS4(5, 2, 8); else FEDAGG_CONV_LDS(5, 2, 16);
       } else {
-        if (plan.cc == 4) {
-          if (plan.xm == 8) FEDAGG_CONV_LDS(3, 4, 8);
-          else if (plan.xm == 12) FEDAGG_CONV_LDS(3, 4, 12);
-          else FEDAGG_CONV_LDS(3, 4, 16);
-        } else {
-          if (plan.xm == 8) FEDAGG_CONV_LDS4(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
-        }
+        if (plan.xm == 8) FEDAGG_CONV_LDS4(3, 2, 8); else FEDAGG_CONV_LDS(3, 2, 16);
       }
 #undef FEDAGG_CONV_FLAT
 #undef FEDAGG_CONV_FLAT_H
