@@ -1413,7 +1413,7 @@ constexpr int kTL_K = 32;  // inputs per LDS stage
 constexpr int kTL_PAD = 1;
 
 constexpr int64_t kTL_WideIn = 1024;  // inputs above which a Linear layer counts as wide
-constexpr size_t kTL_WidePadKB = 20;   // LDS reserved per workgroup of a wide layer: 4 per CU
+constexpr size_t kTL_WidePadKB = 9;    // LDS reserved per workgroup of a wide layer: 6 per CU
 
 // XCD-aware order of a 1-D grid of teacher tiles (the 1-D form of
 // conv_tile_order below): launch index L runs on XCD L % 8, so in plain order
@@ -3229,7 +3229,10 @@ int fedagg_teacher_linear_f32(const float* x, int64_t x_kstride, const float* pa
       // wide layers stream each teacher's W once (weight-bound): at eight
       // workgroups per CU their 2048 concurrent row streams lose DRAM locality
       // (SimpleCNN's fc, in = 3136: 1049 vs 960 us for the generic kernel at
-      // four per CU), so they reserve LDS for four per CU
+      // four per CU), so they reserve LDS for six per CU (round 4, warmed-up
+      // interleaved A/B, profiles/r04w: SimpleCNN fc 0.927 -> 0.905 ms,
+      // SimpleCNN2 fc1 0.523 -> 0.504 ms per 500 teachers against four; five
+      // in between)
       const size_t pad = (in > kTL_WideIn) ? kTL_WidePadKB * 1024 : 0;
       hipLaunchKernelGGL(k_teacher_linear_buf, dim3(static_cast<unsigned>(kn * per)), dim3(256), pad,
                          static_cast<hipStream_t>(stream), x + k0 * x_kstride, x_kstride,
