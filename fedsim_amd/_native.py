@@ -23,8 +23,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
 
 # Must match include/fedagg.h
-ABI_VERSION = 3  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
-#                 3: the rejected flat-load / LDS-weight flag bits refused
+ABI_VERSION = 4  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
+#                 3: the rejected flat-load / LDS-weight flag bits refused;
+#                 4: + fedagg_finalize_f64 (fp64 keys of the generic aggregator)
 FEDAGG_INIT = 0x1
 FEDAGG_FINALIZE = 0x2
 FEDAGG_NT = 0x4
@@ -165,6 +166,11 @@ SIGNATURES = {
     "fedagg_finalize_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p,
+         ctypes.c_void_p],
+    ),
+    "fedagg_finalize_f64": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_void_p,
          ctypes.c_void_p],
     ),
     "fedagg_fedavg_sgd_f32": (

@@ -857,6 +857,22 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const float* acc, float W32
   }
 }
 
+// f64 true division (the fp64 keys of the dtype-generic aggregator); two
+// doubles per lane per iteration, 16-B loads
+__global__ __launch_bounds__(kBlock) void k_finalize_f64(const double* acc, double W,
+                                                         int64_t P, double* out) {
+  using f64x2 = double __attribute__((ext_vector_type(2)));
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t nvec = P / 2;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nvec; i += stride) {
+    f64x2 a = reinterpret_cast<const f64x2*>(acc)[i];
+    a.x = a.x / W;
+    a.y = a.y / W;
+    reinterpret_cast<f64x2*>(out)[i] = a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (P & 1)) out[P - 1] = acc[P - 1] / W;
+}
+
 // torch CPU SGD.step = param.add_(grad, alpha=-lr) = fma(-lr, g, param)
 __device__ __forceinline__ float sgd_rn(float c, float g, float neg_lr) {
   return __builtin_fmaf(neg_lr, g, c);
@@ -3580,6 +3596,15 @@ int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out, void
   if (!acc || !out || !aligned16(acc) || !aligned16(out)) return FEDAGG_EINVAL;
   hipLaunchKernelGGL(k_finalize, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), acc, W32, P, out);
+  return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_finalize_f64(const double* acc, double W, int64_t P, double* out, void* stream) {
+  if (P < 0) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!acc || !out || !aligned16(acc) || !aligned16(out)) return FEDAGG_EINVAL;
+  hipLaunchKernelGGL(k_finalize_f64, dim3(elementwise_grid(P / 2 + 1)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), acc, W, P, out);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -8,6 +8,7 @@ Reference arithmetic each op reproduces bit for bit:
   reduce      SerialAggregator.add   fedsim/utils/aggregators.py:17-40
               (+ FINALIZE: get/pop   fedsim/utils/aggregators.py:56-60,118-122)
   finalize    SerialAggregator.pop   fedsim/utils/aggregators.py:118-122
+  finalize_f64  the same for fp64 sums (the dtype-generic keys)
   fedavg_sgd  FedAvg.optimize        fedsim/distributed/centralized/training/fedavg.py:199-203
   adabest_sgd AdaBest.optimize       fedsim/distributed/centralized/training/adabest.py:178-188
 """
@@ -27,6 +28,7 @@ __all__ = [
     "reduce_slab",
     "reduce_rows",
     "finalize",
+    "finalize_f64",
     "fedavg_sgd",
     "adabest_sgd",
     "tuning_flags",
@@ -566,6 +568,24 @@ def finalize(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.
         acc.data_ptr(), fl32(W), acc.numel(), out.data_ptr(), _stream_ptr(acc.device)
     )
     check(rc, "fedagg_finalize_f32")
+    return out
+
+
+def finalize_f64(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = acc / float(W) in f64 (IEEE true division) — SerialAggregator.pop's
+    ``v / w`` for an fp64 sum (fedagg_finalize_f64)."""
+    if not isinstance(acc, torch.Tensor) or acc.dtype != torch.float64:
+        raise TypeError("acc must be a float64 torch.Tensor")
+    if acc.device.type != "cuda":
+        raise ValueError(f"acc must live on a HIP device, got {acc.device}")
+    if out is None:
+        out = torch.empty_like(acc, memory_format=torch.contiguous_format)
+    if out.dtype != torch.float64 or out.device != acc.device or out.numel() != acc.numel():
+        raise ValueError("out must be a float64 tensor of acc's size on acc's device")
+    rc = _native.load().fedagg_finalize_f64(
+        acc.data_ptr(), float(W), acc.numel(), out.data_ptr(), _stream_ptr(acc.device)
+    )
+    check(rc, "fedagg_finalize_f64")
     return out
 
 

@@ -21,10 +21,27 @@ tensor-valued keys are reduced on the MI355X by libfedagg:
   ``__contains__`` keep the reference semantics; a missing key raises
   ``Exception(f"{key} is not in the aggregator")``.
 
-Python numbers and 0-dim tensors (the per-split scalar metrics that
-serial_aggregation adds, training/utils.py:47-51) stay on the host with the
-reference's own arithmetic.  N-d tensors must be float32: there is no CPU
-fallback for them — without a HIP device / libfedagg the add raises.
+Every other value keeps the reference's own arithmetic, exactly as
+aggregators.py:17-40 writes it (``sum_v + value * weight`` with torch's type
+promotion, on the value's own device):
+
+* Python numbers and 0-dim tensors (the per-split scalar metrics that
+  serial_aggregation adds, training/utils.py:47-51);
+* N-d tensors of any other dtype (fp64, bf16 / fp16, integer, bool): an fp64
+  or bf16 model's parameters, a plugin's per-class counts.  Their ``v / w``
+  at ``get`` / ``pop`` is ATen CPU's true division -- in f64 for an fp64 sum
+  (fedagg_finalize_f64), in f32 for the others (fedagg_finalize_f32), the
+  rounding ATen's CPU kernel gives and torch's own HIP kernel (a multiply by
+  the reciprocal) does not -- so HIP-resident keys match the reference CPU
+  aggregation bit for bit;
+* a tensor key that stops fitting the kernel -- a value of another dtype or
+  shape, a non-real weight, a scalar added to it -- leaves it: its exact
+  running sum so far continues under the reference's arithmetic, so torch's
+  promotion (fp32 sum + fp64 value -> fp64) and broadcasting apply as in the
+  reference.
+
+fp32 N-d tensors have no CPU fallback: without a HIP device / libfedagg the
+add raises.
 """
 from __future__ import annotations
 
@@ -37,6 +54,7 @@ from concurrent.futures import Future, ThreadPoolExecutor
 from concurrent.futures import wait as _wait_futures
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -606,6 +624,84 @@ class _DeviceEntry(_TensorEntry):
         self.acc = None
 
 
+def _kernel_weight(weight) -> bool:
+    """A weight the fp32 kernel applies exactly as the reference's
+    ``value * weight`` does (fl32(weight) * value in fp32): a real Python or
+    numpy number, or a real 0-dim host tensor (None raises in add, as in the
+    reference)."""
+    if weight is None or isinstance(weight, (int, float, np.integer, np.floating)):
+        return True
+    if isinstance(weight, torch.Tensor):
+        # a 0-dim weight does not promote the value's dtype: fp32 * fl32(w)
+        return weight.dim() == 0 and weight.device.type == "cpu" and not weight.is_complex()
+    return False
+
+
+def _kernel_value(value, weight) -> bool:
+    """Whether (value, weight) is the fp32 kernel path's: an fp32 N-d tensor
+    and a real scalar weight."""
+    return (isinstance(value, torch.Tensor) and value.dim() > 0
+            and value.dtype == torch.float32 and _kernel_weight(weight))
+
+
+def reference_add(pair, value, weight):
+    """The reference's ``add`` on one key's (sum, weight) pair
+    (fedsim/utils/aggregators.py:17-40, its evaluation order included):
+    returns the new pair; raises, leaving nothing changed, where it does."""
+    new_v, new_w = (value, None) if weight is None else (value * weight, weight)
+    sum_v, cur_w = pair
+    if (sum_v is None) or (new_v is None):
+        return (sum_v + new_v, None)
+    return (sum_v + new_v, cur_w + new_w)
+
+
+# sums whose ``v / w`` ATen computes in f32 (its opmath type) on the CPU
+_F32_OPMATH = (torch.float32, torch.float16, torch.bfloat16)
+
+
+def reference_quotient(v, w):
+    """The reference's ``v / w`` of get / pop (aggregators.py:58-60,
+    120-122) for a sum ``v`` and a nonzero weight ``w``.  On the host it IS
+    the reference's expression.  For a HIP tensor and a real Python / numpy
+    weight it reproduces ATen CPU's rounding, which torch's HIP kernel (a
+    multiply by the reciprocal) does not: the quotient's dtype is torch's
+    promotion (an integer sum divides into the default float dtype), the
+    division is IEEE true division in ATen's opmath type (f64 for fp64, f32
+    for fp32 / fp16 / bf16) by the weight rounded to that type, then rounded
+    to the quotient's dtype."""
+    if not (isinstance(v, torch.Tensor) and v.device.type == "cuda" and v.dim() > 0
+            and not v.is_complex()):
+        return v / w
+    if isinstance(w, torch.Tensor):
+        # a 0-dim host weight (a tensor-valued running weight) is first cast
+        # to the common dtype, as ATen's TensorIterator does
+        if w.dim() != 0 or w.device.type != "cpu" or w.is_complex():
+            return v / w
+    elif not isinstance(w, (int, float, np.integer, np.floating)):
+        return v / w
+    out = torch.result_type(v, w)
+    if not out.is_floating_point:
+        out = torch.get_default_dtype()  # true division of integers
+    if isinstance(w, torch.Tensor):
+        w = w.to(out).item()
+    if out == torch.float64:
+        x = v.to(torch.float64).contiguous()
+        q = ops.finalize_f64(x if x.data_ptr() % 16 == 0 else x.clone(), w)
+    elif out in _F32_OPMATH:
+        x = v.to(torch.float32).contiguous()
+        q = ops.finalize(x if x.data_ptr() % 16 == 0 else x.clone(), w,
+                         out=torch.empty(x.shape, dtype=torch.float32, device=x.device))
+    else:
+        return v / w
+    return q.view(v.shape).to(out)
+
+
+def _drop_entry(entry) -> None:
+    release = getattr(entry, "release", None)
+    if release is not None:
+        release()
+
+
 class SerialAggregator(object):
     """Device-backed drop-in for the reference SerialAggregator
     (fedsim/utils/aggregators.py:11-144).
@@ -658,8 +754,10 @@ class SerialAggregator(object):
         return _DeviceEntry(value, _hip_device(value, self._opts.device), self._opts, self)
 
     @staticmethod
-    def _is_device_value(value) -> bool:
-        return isinstance(value, torch.Tensor) and value.dim() > 0
+    def _is_device_value(value, weight=1) -> bool:
+        """Whether an add of (value, weight) to a new key starts a kernel
+        entry (an fp32 N-d tensor with a real scalar weight)."""
+        return _kernel_value(value, weight)
 
     def reserve(self, key, P: int, device) -> Optional[SlabRow]:
         """A row of ``key``'s HBM ring for a client to write its P-parameter
@@ -691,9 +789,9 @@ class SerialAggregator(object):
 
     def add(self, key, value, weight=None):
         entry = self._members.get(key)
-        if entry is None and key in self._reserved and self._is_device_value(value):
+        if entry is None and key in self._reserved:
             res = self._reserved.pop(key)
-            if tuple(value.shape) == res.shape:
+            if self._is_device_value(value, weight) and tuple(value.shape) == res.shape:
                 # the first add defines the key, as in the reference: adopt
                 # the reserved ring only for a value of its shape
                 entry = self._members[key] = res
@@ -701,24 +799,25 @@ class SerialAggregator(object):
             else:
                 res.release()  # a reserved row still alive keeps a copy
         if isinstance(entry, _TensorEntry):
-            if not self._is_device_value(value):
-                raise TypeError(f"key {key!r} aggregates tensors; got {type(value).__name__}")
-            entry.add(value, weight)
+            if self._is_device_value(value, weight) and tuple(value.shape) == entry.shape:
+                entry.add(value, weight)
+                return
+            # the key leaves the kernel path (a value of another dtype or
+            # shape, a scalar, a non-real weight): its exact running sum so
+            # far continues under the reference's arithmetic, which applies
+            # torch's promotion / broadcasting -- or raises -- as there
+            pair = reference_add((entry.get_sum(), entry.cur_w), value, weight)
+            _drop_entry(entry)
+            self._members[key] = pair
             return
-        if entry is None and self._is_device_value(value):
+        if entry is None and self._is_device_value(value, weight):
             entry = self._new_entry(value)
             entry.add(value, weight)
             self._members[key] = entry
             return
-        if entry is not None and self._is_device_value(value):
-            raise TypeError(f"key {key!r} aggregates scalars; got an N-d tensor")
-        # host path: the reference's own arithmetic (aggregators.py:17-40)
-        new_v, new_w = (value, None) if weight is None else (value * weight, weight)
-        sum_v, cur_w = self._members.get(key, (0, 0))
-        if (sum_v is None) or (new_v is None):
-            self._members[key] = (sum_v + new_v, None)
-        else:
-            self._members[key] = (sum_v + new_v, cur_w + new_w)
+        # the reference's own arithmetic (aggregators.py:17-40) on the
+        # value's device: scalars, 0-dim and non-fp32 tensors
+        self._members[key] = reference_add(self._members.get(key, (0, 0)), value, weight)
 
     def _entry(self, key):
         if key not in self._members:
@@ -732,7 +831,7 @@ class SerialAggregator(object):
         v, w = e
         if w is None or w == 0:
             return v
-        return v / w
+        return reference_quotient(v, w)
 
     def get_sum(self, key):
         e = self._entry(key)
@@ -757,7 +856,7 @@ class SerialAggregator(object):
         v, w = e
         if w is None or w == 0:
             return v
-        return v / w
+        return reference_quotient(v, w)
 
     def pop_device(self, key):
         """``pop`` that leaves a tensor result in HBM (no D2H), for the fused

@@ -14,7 +14,7 @@
  *                                                  fedsim/utils/aggregators.py:56-60,118-122
  *   fedagg_reduce_blocked_f32
  *       same, over a column-blocked HBM slab layout
- *   fedagg_finalize_f32
+ *   fedagg_finalize_f32 / fedagg_finalize_f64
  *       replaces SerialAggregator.get/pop's v / w  fedsim/utils/aggregators.py:56-60,118-122
  *   fedagg_fedavg_sgd_f32
  *       replaces FedAvg.optimize's pseudo-grad + torch.optim.SGD.step
@@ -60,8 +60,9 @@ extern "C" {
    (linear, conv2d, pad-LRN-maxpool) and slab-row (pack_segments, unpack_row)
    entry points and their structs; 3: flag bits 0x10000 / 0x20000 (the
    flat-load and LDS-weight A/B switches, measured and rejected) are no
-   longer accepted (FEDAGG_EINVAL) */
-#define FEDAGG_ABI_VERSION 3
+   longer accepted (FEDAGG_EINVAL); 4: + fedagg_finalize_f64 (the reference's
+   v / w for fp64 keys of the dtype-generic SerialAggregator) */
+#define FEDAGG_ABI_VERSION 4
 
 /* flags for the reduce entry points */
 #define FEDAGG_INIT      0x1  /* ignore acc_in: start from +0.0f (first batch of a round) */
@@ -321,6 +322,17 @@ int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, in
 
 /* out[p] = fl32(acc[p] / W32)  (IEEE true division; out may alias acc). */
 int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out,
+                        void* stream);
+
+/*
+ * out[p] = acc[p] / W  in f64 (IEEE true division; out may alias acc).
+ * SerialAggregator.get/pop's  v / w  for an fp64 sum (aggregators.py:56-60,
+ * 118-122): ATen's CPU true division by a Python scalar is a / (double)w,
+ * while torch's HIP kernel multiplies by the reciprocal, which is not the
+ * reference's rounding.  Bf16 / fp16 / integer sums divide in f32
+ * (fedagg_finalize_f32 on the converted sum, as ATen's opmath does).
+ */
+int fedagg_finalize_f64(const double* acc, double W, int64_t P, double* out,
                         void* stream);
 
 /*

@@ -40,16 +40,22 @@ class ReferenceSerialAggregator(object):
     (fedsim/utils/aggregators.py:11-144): per key, ``value * weight`` added to
     the running sum (first add: ``0 + tensor``), the Python weight sum, and
     ``sum / weight`` on get / pop (the raw sum for a zero / None weight).
-    TEST / MEASUREMENT INFRASTRUCTURE: the reference leg of
-    tools/bench_host_rounds.py."""
+    Any value type torch arithmetic accepts (fp64 / bf16 / integer tensors,
+    Python numbers).  TEST / MEASUREMENT INFRASTRUCTURE: the reference leg of
+    tools/bench_host_rounds.py and the checker of the dtype-generic keys
+    (tests/test_generic_keys.py, pinned to tests/golden/generic_keys.*)."""
 
     def __init__(self) -> None:
         self._members = dict()
 
     def add(self, key, value, weight=None):
-        new_v = value * weight if weight is not None else value
+        # aggregators.py:17-21 (_get_pair) and :35-40, in the reference's order
+        new_v, new_w = (value, None) if weight is None else (value * weight, weight)
         sum_v, cur_w = self._members.get(key, (0, 0))
-        self._members[key] = (sum_v + new_v, cur_w + weight)
+        if (sum_v is None) or (new_v is None):
+            self._members[key] = (sum_v + new_v, None)
+        else:
+            self._members[key] = (sum_v + new_v, cur_w + new_w)
 
     def get(self, key):
         if key not in self._members:

@@ -74,6 +74,26 @@ class TinyModel(nn.Module):
         return self.l2(torch.relu(self.l1(x)))
 
 
+class TinyModel64(TinyModel):
+    """TinyModel in float64 (a model built under torch.set_default_dtype(
+    torch.float64)): its parameter vector is an fp64 key of the aggregator."""
+
+    def __init__(self):
+        super().__init__()
+        self.double()
+
+
+class TinyModelBF16(TinyModel):
+    """TinyModel in bfloat16."""
+
+    def __init__(self):
+        super().__init__()
+        self.to(torch.bfloat16)
+
+
+MODELS = {"TinyModel": TinyModel, "TinyModel64": TinyModel64, "TinyModelBF16": TinyModelBF16}
+
+
 def synthetic_send_to_server(id, rounds, storage, datasets, train_split_name, scores, epochs,
                              criterion, train_batch_size, inference_batch_size, optimizer_def,
                              lr_scheduler_def=None, device="cuda", ctx=None,
@@ -81,7 +101,7 @@ def synthetic_send_to_server(id, rounds, storage, datasets, train_split_name, sc
     model = ctx["model"]
     base = parameters_to_vector(model.parameters()).detach().cpu()
     delta = torch.from_numpy((0.01 * V.gauss(id * 7919 + rounds, base.numel())).astype(np.float32))
-    local = base + delta
+    local = base + delta.to(base.dtype)  # the model's dtype (a no-op for fp32 models)
     n = len(datasets[train_split_name])
     return dict(
         local_params=local.to(device),

@@ -1,0 +1,165 @@
+"""The dtype-generic drop-in SerialAggregator against the REFERENCE's own
+transcripts (tests/golden/generic_keys.json, tools/gen_golden_generic.py).
+
+fp32 N-d tensor keys run on the HIP kernels; every other value (fp64, bf16 /
+fp16, integer and bool tensors, scalars, and tensor keys that stop fitting
+the kernel) keeps the reference's arithmetic (fedsim/utils/aggregators.py:
+17-40, 42-60, 104-122).  Each scenario of oracle/generic_cases.py must give
+the reference's transcript bit for bit: every get / get_sum / get_weight /
+pop / pop_all result (dtype, shape, bytes), every exception type.
+
+CPU tests: the oracle restatement against the reference transcripts, the
+drop-in on scenarios that never start a kernel key, and the fp64 / bf16
+round loops on device="cpu".  GPU tests: every scenario with values on the
+host and in HBM, and the same round loops with the cloud in HBM.
+"""
+import json
+import os
+import random
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN_DIR
+from oracle import generic_cases as G
+from oracle import synthetic_fl as S
+from oracle.reference_loop import ReferenceSerialAggregator
+
+with open(os.path.join(GOLDEN_DIR, "generic_keys.json")) as _f:
+    _GOLD = json.load(_f)
+SCEN = G.scenarios()
+NAMES = sorted(SCEN)
+HOST_NAMES = [n for n in NAMES if not G.needs_kernel(SCEN[n])]
+RUNS = _GOLD["dtype_runs"]
+
+
+def _decode(rec):
+    return torch.frombuffer(bytearray(__import__("base64").b64decode(rec["b64"])),
+                            dtype=torch.uint8).view(getattr(torch, rec["t"])).reshape(rec["shape"])
+
+
+def test_golden_covers_every_scenario():
+    assert sorted(_GOLD["transcripts"]) == NAMES
+    # the fixtures exercise what they claim: tensor results of every dtype
+    seen = set()
+    for tr in _GOLD["transcripts"].values():
+        for status, rec in tr:
+            if status == "ok" and "t" in rec:
+                seen.add(rec["t"])
+    assert {"float64", "float32", "bfloat16", "float16", "int64", "int32"} <= seen
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_restatement_matches_reference(name):
+    assert G.replay(ReferenceSerialAggregator(), SCEN[name]) == _GOLD["transcripts"][name]
+
+
+@pytest.mark.parametrize("name", HOST_NAMES)
+def test_dropin_generic_keys_host(name):
+    from fedsim_amd.utils import SerialAggregator
+
+    assert G.replay(SerialAggregator(), SCEN[name]) == _GOLD["transcripts"][name]
+
+
+def _round(run, device):
+    from fedsim_amd.distributed.centralized import training
+
+    cls = S.make_algorithm(getattr(training, run["algorithm"]))
+    random.seed(S.RANDOM_SEED)
+    torch.manual_seed(S.TORCH_SEED)
+    alg = cls(data_manager=S.FakeDataManager(), metric_logger=None, num_clients=S.NUM_CLIENTS,
+              sample_scheme="uniform", sample_rate=S.SAMPLE_RATE,
+              model_def=S.MODELS[run["model"]], epochs=1, criterion_def="CrossEntropyScore",
+              optimizer_def=partial(torch.optim.SGD, **run["opt_kwargs"]), device=device,
+              **run["alg_kwargs"])
+    scores = alg.train(rounds=S.ROUNDS)
+    st = alg.get_server_storage()
+    cloud = st.read("cloud_params")
+    got = dict(cloud=cloud.detach())
+    if run["algorithm"] == "AdaBest":
+        got["avg_params"] = st.read("avg_params")
+    buf = st.read("optimizer").state[cloud].get("momentum_buffer")
+    if buf is not None:
+        got["momentum_buffer"] = buf
+    return got, scores
+
+
+@pytest.mark.parametrize("run", RUNS, ids=[f"{r['id']}-{r['algorithm']}-{r['model']}"
+                                           for r in RUNS])
+def test_dtype_round_loop_host(run):
+    """The round driver with an fp64 / bf16 model on device="cpu": the
+    server state after 5 rounds equals the reference's bit for bit (the
+    fused fp32 step is off for these dtypes: torch.optim's route)."""
+    got, scores = _round(run, "cpu")
+    assert got.keys() == run["outputs"].keys()
+    for k, t in got.items():
+        assert t.device.type == "cpu"
+        assert G.encode(t) == run["outputs"][k], k
+    assert {k: G.encode(v) for k, v in scores.items()} == run["scores"]
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("name", NAMES)
+def test_dropin_generic_keys_gpu(name, where):
+    """Every scenario with a GPU present: fp32 keys on the HIP kernel (and
+    leaving it when a value no longer fits), values on the host or in HBM;
+    the quotients of HIP-resident generic keys through fedagg_finalize_f32 /
+    _f64.  Bitwise the reference's transcript."""
+    from fedsim_amd.utils import SerialAggregator
+
+    assert torch.cuda.is_available()
+    dev = torch.device("cuda:0") if where == "device" else None
+    got = G.replay(SerialAggregator(max_rows=2), SCEN[name], device=dev)
+    assert got == _GOLD["transcripts"][name]
+
+
+@pytest.mark.gpu
+def test_hip_quotient_is_cpu_true_division():
+    """reference_quotient on HIP tensors reproduces ATen CPU's ``v / w``
+    (torch's HIP division by a scalar multiplies by the reciprocal)."""
+    from fedsim_amd.utils.aggregators import reference_quotient
+
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(7)
+    for dt in (torch.float64, torch.float32, torch.bfloat16, torch.float16, torch.int64):
+        if dt.is_floating_point:
+            v = (torch.randn(4099, generator=g, dtype=torch.float64) * 1e3).to(dt)
+        else:
+            v = torch.randint(-10**9, 10**9, (4099,), generator=g, dtype=dt)
+        for w in (3, 7.3, 0.1, 1e-3, 123456.789, 2 ** 31 + 5, np.float32(0.7), torch.tensor(2.5)):
+            want = v / w
+            q = reference_quotient(v.to(dev), w)
+            assert q.dtype == want.dtype and q.device == dev
+            assert torch.equal(q.cpu().view(-1).view(torch.uint8),
+                               want.view(-1).view(torch.uint8)), (dt, w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run", RUNS, ids=[f"{r['id']}-{r['algorithm']}-{r['model']}"
+                                           for r in RUNS])
+@pytest.mark.parametrize("device", ["cpu", "cuda"])
+def test_dtype_round_loop_gpu(run, device):
+    """The same fp64 / bf16 rounds with a GPU present.  device="cpu": bitwise
+    (every server op is the reference's CPU arithmetic or a bit-exact HIP
+    quotient).  device="cuda": the aggregation is bitwise by construction,
+    but torch's own HIP SGD step (add_ with alpha, momentum) may contract
+    differently from the CPU's: bitwise for plain SGD at lr=1 (one exact
+    rounding either way), else within 1e-12 (fp64) relative."""
+    got, scores = _round(run, device)
+    plain = run["opt_kwargs"] == dict(lr=1.0) and run["algorithm"] == "FedAvg"
+    for k, t in got.items():
+        assert t.device.type == device
+        want = _decode(run["outputs"][k])
+        if device == "cpu" or plain:
+            assert G.encode(t) == run["outputs"][k], k
+        else:
+            err = (t.cpu().double() - want.double()).norm() / want.double().norm()
+            print(run["id"], k, "rel err", float(err), "bitwise", G.encode(t) ==
+                  run["outputs"][k])
+            assert err <= 1e-12, k
+    if device == "cpu" or plain:
+        assert {k: G.encode(v) for k, v in scores.items()} == run["scores"]

@@ -185,8 +185,13 @@ def test_aggregator_semantics_on_device(dev):
         agg.pop("t")
     with pytest.raises(TypeError):
         agg.add("u", torch.ones(4), None)
-    with pytest.raises(TypeError):
-        agg.add("v", torch.ones(4, dtype=torch.float64), 1)
+    # non-fp32 tensors keep the reference's arithmetic (aggregators.py:17-40):
+    # the full scenario set is tests/test_generic_keys.py
+    v = torch.arange(4, dtype=torch.float64)
+    agg.add("v", v, 3)
+    agg.add("v", 2 * v, 1)
+    got = agg.pop("v")
+    assert got.dtype == torch.float64 and torch.equal(got, (0 + v * 3 + 2 * v * 1) / 4)
     # weights summing to zero -> raw sum (aggregators.py:56-57)
     agg.add("z", torch.ones(4), 2)
     agg.add("z", torch.ones(4), -2)
