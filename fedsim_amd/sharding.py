@@ -163,7 +163,9 @@ def weights_fp32(weights: Sequence, device) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 # plugin surface: a parameter-sharded SerialAggregator
 # ---------------------------------------------------------------------------
-from .utils.aggregators import SerialAggregator, _DeviceEntry, _hip_device, _TensorEntry  # noqa: E402
+from .utils.aggregators import (  # noqa: E402
+    SerialAggregator, _DeviceEntry, _hip_device, _kernel_value, _TensorEntry, reference_add,
+    reference_quotient)
 
 
 def _group_rank_world(group):
@@ -661,6 +663,107 @@ class _ClientShardEntry(_TensorEntry):
         self.agg._apply_step(step, avg)
 
 
+def _meta(x):
+    """The shape / dtype stand-in of a value in the replicated ``add``: the
+    reference's arithmetic on meta tensors gives the running sum's promotion,
+    broadcasting and errors on every rank without its data (0-dim host
+    tensors and Python numbers are themselves)."""
+    if isinstance(x, torch.Tensor) and not (x.dim() == 0 and x.device.type == "cpu"):
+        return torch.empty(x.shape, dtype=x.dtype, device="meta")
+    return x
+
+
+class _ClientShardRef(_TensorEntry):
+    """A tensor key of a client-sharded round that keeps the reference's
+    arithmetic (aggregators.py:17-40): non-fp32 values (an fp64 / bf16
+    model, integer counts), or an fp32 key that stopped fitting the kernel.
+
+    Every rank replays each ``add`` on meta tensors, so all of them know the
+    running sum's dtype and shape after every row -- and raise together
+    where the reference raises.  A rank keeps ``value * weight`` of its own
+    rows (the reference's product, computed at add on the value's device).
+    The sum is formed in arrival order through the ranks (the chain in
+    either client_reduction mode: the adds of a generic sum are not
+    reassociated): rank r receives the running sum of the ranks before it,
+    adds its products one by one as the reference does, and passes it on;
+    the last holder broadcasts it.  Tensors travel as raw bytes (any dtype,
+    gloo or RCCL).  After a get / get_sum the global sum becomes the base
+    that later adds continue."""
+
+    def __init__(self, agg: "ClientShardedSerialAggregator", key, base=(0, 0), src_type="cpu"):
+        self.agg = agg
+        self._key = key
+        self.base, self.cur_w = base
+        self.meta = _meta(self.base)
+        self.rows = []    # this rank's products value * weight, in arrival order
+        self.owners = []  # ranks holding rows, in arrival order (one run each)
+        self.after = []   # meta of the running sum after each owner's run
+        self.dev = agg._reduce_device()
+        self.out_device = self.dev if src_type == "cuda" else torch.device("cpu")
+
+    def add(self, value, weight) -> None:
+        meta, new_w = reference_add((self.meta, self.cur_w), _meta(value), weight)
+        remote = isinstance(value, RemoteRow)
+        owner = value.owner if remote else self.agg.rank
+        if not (remote or (isinstance(value, torch.Tensor) and value.dim() > 0)):
+            # a scalar, held by every rank: it joins the base before any row,
+            # else the run of the rank whose rows precede it
+            if not self.owners:
+                self.base = self.base + (value if weight is None else value * weight)
+                self.meta, self.cur_w = _meta(self.base), new_w
+                return
+            owner = self.owners[-1]
+        if owner == self.agg.rank:
+            self.rows.append(value if weight is None else value * weight)
+        if not self.owners or self.owners[-1] != owner:
+            self.owners.append(owner)
+            self.after.append(meta)
+        else:
+            self.after[-1] = meta
+        self.meta, self.cur_w = meta, new_w
+
+    def _global_sum(self):
+        """Collective: the reference's running sum over every rank's rows."""
+        def local(acc):
+            for nv in self.rows:
+                if isinstance(acc, torch.Tensor) and isinstance(nv, torch.Tensor) and \
+                        acc.dim() > 0 and acc.device != nv.device:
+                    acc = acc.to(nv.device)
+                acc = acc + nv
+            return acc
+
+        if self.agg._solo or not self.owners:
+            s = local(self.base)
+        else:
+            s = self.agg._ordered_reference_sum(self.owners, self.after, self.base, local)
+        # later adds continue this sum (identical on every rank)
+        self.base, self.meta = s, _meta(s)
+        self.rows, self.owners, self.after = [], [], []
+        return s
+
+    def _deliver(self, t):
+        if isinstance(t, torch.Tensor) and t.dim() > 0 and t.device != self.out_device:
+            t = t.to(self.out_device)
+        return t
+
+    def _weighted(self) -> bool:
+        return not (self.cur_w is None or self.cur_w == 0)
+
+    def get_sum(self):
+        return self._deliver(self._global_sum())
+
+    def get(self):
+        s = self._global_sum()
+        return self._deliver(reference_quotient(s, self.cur_w) if self._weighted() else s)
+
+    def pop(self, on_device: bool = False):
+        return self.get()
+
+    def pop_step(self, step: ops.ServerStep) -> None:
+        avg = self.get()
+        self.agg._apply_step(step, avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+
+
 class ClientShardedSerialAggregator(SerialAggregator):
     """Client-sharded drop-in for the reference SerialAggregator
     (fedsim/utils/aggregators.py:11-144) for a round loop whose clients are
@@ -804,6 +907,46 @@ class ClientShardedSerialAggregator(SerialAggregator):
         _broadcast(buf, _global_rank(self._group, owners[-1]), self._group)
         return buf
 
+    def _wire_device(self) -> torch.device:
+        if dist.get_backend(self._group) == dist.Backend.GLOO:
+            return torch.device("cpu")
+        return self._reduce_device()
+
+    def _ordered_reference_sum(self, owners, after, base, local):
+        """Collective: the running sum of a _ClientShardRef key through the
+        ranks in ``owners`` order (``after[i]``: the sum's meta after owner
+        i's run; ``local(acc)`` adds this rank's products onto ``acc``), then
+        broadcast from the last owner.  Sums travel as raw bytes."""
+        if len(set(owners)) != len(owners):
+            raise RuntimeError("a client-sharded round needs each rank's clients to be one "
+                               "contiguous run of the round's arrival order")
+        me, wire = self.rank, self._wire_device()
+
+        def empty_like_meta(m):
+            return torch.empty(m.numel() * m.element_size(), dtype=torch.uint8, device=wire)
+
+        def as_bytes(t):
+            return t.to(wire).contiguous().reshape(-1).view(torch.uint8)
+
+        def from_bytes(b, m):
+            return b.view(m.dtype).reshape(m.shape)
+
+        s = None
+        if me in owners:
+            i = owners.index(me)
+            acc = base
+            if i > 0:
+                buf = empty_like_meta(after[i - 1])
+                _recv(buf, _global_rank(self._group, owners[i - 1]), self._group)
+                acc = from_bytes(buf, after[i - 1])
+            s = local(acc)
+            if i + 1 < len(owners):
+                _send(as_bytes(s), _global_rank(self._group, owners[i + 1]), self._group)
+        last = after[-1]
+        buf = as_bytes(s) if me == owners[-1] else empty_like_meta(last)
+        _broadcast(buf, _global_rank(self._group, owners[-1]), self._group)
+        return from_bytes(buf, last)
+
     def divide(self, s: torch.Tensor, W) -> torch.Tensor:
         """fl32(s / fl32(W)), the reference's ``get`` divide."""
         if s.device.type == "cuda":
@@ -854,20 +997,39 @@ class ClientShardedSerialAggregator(SerialAggregator):
             step.apply(avg if avg.device == step.cloud.device else avg.to(step.cloud.device))
 
     def add(self, key, value, weight=None):
-        if isinstance(value, torch.Tensor) and value.dim() > 0:
-            e = self._members.get(key)
-            if e is None:
-                src = value.src_type if isinstance(value, RemoteRow) else value.device.type
-                e = _ClientShardEntry(self, value.shape, src)
-                e._key = key
-                e.add(value, weight)  # may raise (weight None): the key is not created
-                self._members[key] = e
-                return
-            if not isinstance(e, _ClientShardEntry):
-                raise TypeError(f"key {key!r} aggregates scalars; got an N-d tensor")
+        """Every rank makes the same choice (the values' dtypes and shapes
+        and the weights are known everywhere): fp32 tensors with real
+        weights go to the exact HIP rows (_ClientShardEntry); anything else
+        keeps the reference's arithmetic (_ClientShardRef), continuing a
+        kernel key's exact sum when a value stops fitting it."""
+        e = self._members.get(key)
+        tensor = isinstance(value, torch.Tensor) and value.dim() > 0
+        if not tensor and not isinstance(e, _TensorEntry):
+            super().add(key, value, weight)  # scalar key: the host arithmetic
+            return
+        src = value.src_type if isinstance(value, RemoteRow) else \
+            value.device.type if tensor else "cpu"
+        if isinstance(e, _ClientShardEntry) and _kernel_value(value, weight) and \
+                tuple(value.shape) == e.shape:
             e.add(value, weight)
             return
-        super().add(key, value, weight)
+        if e is None and _kernel_value(value, weight):
+            e = _ClientShardEntry(self, value.shape, src)
+            e._key = key
+            e.add(value, weight)  # may raise (weight None): the key is not created
+            self._members[key] = e
+            return
+        if isinstance(e, _ClientShardEntry):
+            # leave the kernel: the exact sum so far (collective, every rank
+            # reaches this add) is the base of the reference arithmetic
+            e = self._members[key] = _ClientShardRef(self, key, (e.get_sum(), e.cur_w),
+                                                     src_type=e.src_type)
+        if isinstance(e, _ClientShardRef):
+            e.add(value, weight)  # raises as the reference's add would
+            return
+        r = _ClientShardRef(self, key, e if e is not None else (0, 0), src_type=src)
+        r.add(value, weight)  # may raise: the key stays as it was
+        self._members[key] = r
 
     def exchange(self, local_msgs: dict, n: int, failed: bool = False, extras=None):
         """Every rank's client messages of this round, position by position:

@@ -146,6 +146,11 @@ def scenarios() -> Dict[str, List[tuple]]:
     return sc
 
 
+def n_tensor_adds(steps) -> int:
+    return sum(1 for s in steps if s[0] == "add" and isinstance(s[2], ValueSpec)
+               and len(s[2].shape) > 0)
+
+
 def needs_kernel(steps) -> bool:
     """Whether a scenario starts a key on the HIP kernel path (an fp32 N-d
     tensor as a key's first value): on a host without a GPU fedsim_amd
@@ -186,10 +191,13 @@ def encode(x):
     return {"repr": repr(x)}
 
 
-def replay(agg, steps, device=None) -> list:
+def replay(agg, steps, device=None, wrap=None) -> list:
     """Run ``steps`` on ``agg`` (tensor values moved to ``device`` when given)
-    and return the transcript."""
+    and return the transcript.  ``wrap(j, t)``: what the j-th N-d tensor
+    value of the scenario is handed over as (a client-sharded round passes
+    another rank's vectors as stand-ins)."""
     out = []
+    j = 0
     for st in steps:
         op = st[0]
         try:
@@ -199,6 +207,9 @@ def replay(agg, steps, device=None) -> list:
                     value = value.build()
                     if device is not None:
                         value = value.to(device)
+                    if wrap is not None and value.dim() > 0:
+                        value = wrap(j, value)
+                        j += 1
                 if isinstance(weight, ValueSpec):
                     weight = weight.build()  # 0-dim host tensor weights stay on the host
                 agg.add(key, value, weight)

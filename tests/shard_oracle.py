@@ -26,8 +26,9 @@ class OracleEntry(_TensorEntry):
         new_w = self.cur_w + weight
         CALLS["add"] += 1
         # snapshot, as the HIP entry does at add time
-        self.rows.append(np.array(value.detach().cpu().numpy(), dtype=np.float32, copy=True))
-        self.ws.append(weight)
+        self.rows.append(np.array(value.detach().cpu().numpy(), dtype=np.float32,
+                                  copy=True).reshape(-1))
+        self.ws.append(float(weight))  # a 0-dim weight tensor's value, as fl32 takes it
         self.cur_w = new_w
 
     def _weighted(self):

@@ -35,11 +35,6 @@ HOST_NAMES = [n for n in NAMES if not G.needs_kernel(SCEN[n])]
 RUNS = _GOLD["dtype_runs"]
 
 
-def _decode(rec):
-    return torch.frombuffer(bytearray(__import__("base64").b64decode(rec["b64"])),
-                            dtype=torch.uint8).view(getattr(torch, rec["t"])).reshape(rec["shape"])
-
-
 def test_golden_covers_every_scenario():
     assert sorted(_GOLD["transcripts"]) == NAMES
     # the fixtures exercise what they claim: tensor results of every dtype
@@ -143,23 +138,13 @@ def test_hip_quotient_is_cpu_true_division():
                                            for r in RUNS])
 @pytest.mark.parametrize("device", ["cpu", "cuda"])
 def test_dtype_round_loop_gpu(run, device):
-    """The same fp64 / bf16 rounds with a GPU present.  device="cpu": bitwise
-    (every server op is the reference's CPU arithmetic or a bit-exact HIP
-    quotient).  device="cuda": the aggregation is bitwise by construction,
-    but torch's own HIP SGD step (add_ with alpha, momentum) may contract
-    differently from the CPU's: bitwise for plain SGD at lr=1 (one exact
-    rounding either way), else within 1e-12 (fp64) relative."""
+    """The same fp64 / bf16 rounds with a GPU present, server state on the
+    host or in HBM: bitwise the reference's (the aggregation and its
+    quotient are bit-exact by construction; torch's own HIP SGD step -- add_
+    with alpha, the momentum update -- measured bitwise to the CPU's for
+    these runs, r05a)."""
     got, scores = _round(run, device)
-    plain = run["opt_kwargs"] == dict(lr=1.0) and run["algorithm"] == "FedAvg"
     for k, t in got.items():
         assert t.device.type == device
-        want = _decode(run["outputs"][k])
-        if device == "cpu" or plain:
-            assert G.encode(t) == run["outputs"][k], k
-        else:
-            err = (t.cpu().double() - want.double()).norm() / want.double().norm()
-            print(run["id"], k, "rel err", float(err), "bitwise", G.encode(t) ==
-                  run["outputs"][k])
-            assert err <= 1e-12, k
-    if device == "cpu" or plain:
-        assert {k: G.encode(v) for k, v in scores.items()} == run["scores"]
+        assert G.encode(t) == run["outputs"][k], k
+    assert {k: G.encode(v) for k, v in scores.items()} == run["scores"]
