@@ -45,7 +45,10 @@ def _to_host(obj):
 def _from_host(obj, device):
     if isinstance(obj, tuple) and len(obj) == 4 and obj[0] == "__fedsim_tensor__":
         _, t, kind, rg = obj
-        t = t.to(device) if kind == "cuda" and device.type == "cuda" else t
+        if kind == "cuda" and device.type == "cuda":
+            # detached first: the host copy may already require grad, and a
+            # copy of it would be a non-leaf (no .grad, refused by optimizers)
+            t = t.detach().to(device)
         return t.requires_grad_(rg) if rg else t
     return obj
 
@@ -108,6 +111,13 @@ def _changed_keys(st: Storage, state) -> list:
         elif not isinstance(obj, (torch.Tensor, type(None), bool, int, float, str, tuple)):
             out.append(k)  # a mutable object: it may have changed in place
     return out
+
+
+def _removed_keys(st: Storage, state) -> list:
+    """Entries the client's storage held before the round and no longer does
+    (Storage.remove)."""
+    items, _ = state
+    return [k for k in items if k not in st._storage]
 
 
 def _distributed_rank() -> int:
@@ -493,18 +503,21 @@ class CentralFLAlgorithm(object):
         mine = {}
         for cid, state in trained:
             st = self._client_memory[cid]
-            keys = _changed_keys(st, state)
-            if keys:
-                mine[cid] = [(k, _to_host(st._storage[k][0]), st._storage[k][1],
-                              st._storage[k][2]) for k in keys]
+            keys, gone = _changed_keys(st, state), _removed_keys(st, state)
+            if keys or gone:
+                mine[cid] = ([(k, _to_host(st._storage[k][0]), st._storage[k][1],
+                               st._storage[k][2]) for k in keys], gone)
         every = [None] * agg.world_size
         dist.all_gather_object(every, mine, group=agg._group)
         for r, mem in enumerate(every):
             if r == agg.rank:
                 continue
-            for cid, items in mem.items():
+            for cid, (items, gone) in mem.items():
                 st = self._client_memory[cid]
                 pending = self._client_on_host.setdefault(cid, {})
+                for k in gone:  # Storage.remove on the rank that trained it
+                    st._storage.pop(k, None)
+                    pending.pop(k, None)
                 for k, obj, rp, wp in items:
                     pending.pop(k, None)
                     if isinstance(obj, tuple) and len(obj) == 4 and obj[0] == "__fedsim_tensor__":

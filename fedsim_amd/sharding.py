@@ -960,14 +960,16 @@ class ClientShardedSerialAggregator(SerialAggregator):
         reference's ``add(x, 1)`` x K order (FedDF's teacher targets,
         feddf.py:120-126) -- or reordered under ``allreduce``."""
         dev = self._reduce_device()
-        local_partial = None
+        local_partial, chainable = None, True
         if rows is not None and rows.shape[0] > 0:
             if self._entry_factory is not None:
-                def local_partial(acc_in):
-                    e = self._entry_factory(rows[0], self)
-                    for r in rows:
-                        e.add(r, 1)
-                    return e.partial(acc_in)
+                # filled before the chain starts, so its feasibility is part of
+                # the collective check (every rank raises together, none waits)
+                e = self._entry_factory(rows[0], self)
+                for r in rows:
+                    e.add(r, 1)
+                chainable = getattr(e, "chainable", lambda: True)()
+                local_partial = e.partial
             else:
                 def local_partial(acc_in):
                     X = rows if rows.device == dev else rows.to(dev)
@@ -975,7 +977,7 @@ class ClientShardedSerialAggregator(SerialAggregator):
                     out = torch.empty(n, dtype=torch.float32, device=dev)
                     ones = torch.ones(X.shape[0], dtype=torch.float32, device=dev)
                     return ops.reduce_slab(X, ones, out, acc_in=acc_in)
-        return self._ordered_sum(owners, local_partial, n)
+        return self._ordered_sum(owners, local_partial, n, chainable)
 
     def broadcast_from(self, t: torch.Tensor, src: int) -> torch.Tensor:
         """Collective: ``t`` on rank ``src`` copied into ``t`` on every rank

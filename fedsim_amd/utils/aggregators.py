@@ -122,8 +122,11 @@ class _Ingest(object):
     the pageable-to-pinned copy and the DMA then run while the next client
     trains instead of between the two clients (tools/bench_host_rounds.py:
     0.2-1.5 ms per client on the critical path otherwise).  A handed-over
-    vector changed in place before its copy ran is caught by its version
-    counter and raised at the round's reduction."""
+    vector changed in place (an in-place torch op: its version counter) from
+    ``add`` until its copy has completed -- the memmove into staging, or for
+    a pinned source the DMA straight from it -- is caught: the counter is
+    checked before and after the copy, and the error is raised at the
+    round's reduction.  A change after that point cannot alter the row."""
 
     def __init__(self, dev: torch.device, nslots: int = _STAGING_SLOTS):
         self.dev = dev
@@ -160,12 +163,16 @@ class _Ingest(object):
         with self.lock:
             return self._put_locked(src, Xb, r, wait_event, version)
 
-    def _put_locked(self, src, Xb, r, wait_event, version):
+    @staticmethod
+    def _check_version(src, version):
         if version is not None and src._version != version:
             raise RuntimeError(
                 "a host client tensor was modified in place after SerialAggregator.add(); "
                 "an aggregator created with borrow=True copies it after add returns (use "
                 "borrow=False to snapshot it at add time)")
+
+    def _put_locked(self, src, Xb, r, wait_event, version):
+        self._check_version(src, version)
         i = self.i % len(self.events)
         self.i += 1
         if self.events[i] is not None:
@@ -183,6 +190,7 @@ class _Ingest(object):
                 ctypes.memmove(host.data_ptr(), src.data_ptr(), 4 * P)
             else:
                 host.copy_(src)
+            self._check_version(src, version)  # not changed while it was copied
         with torch.cuda.stream(self.stream):
             dslot.copy_(host, non_blocking=True)
         if wait_event is not None:
@@ -191,10 +199,12 @@ class _Ingest(object):
         ev = torch.cuda.Event()
         ev.record(self.stream)
         self.events[i] = ev
-        if host is src and version is None:
+        if host is src:
             # the snapshot is complete once the DMA is: the caller may reuse
-            # its pinned buffer after add returns
+            # its pinned buffer after add returns (a handed-over one: checked
+            # once the DMA has read it, on the worker thread)
             ev.synchronize()
+            self._check_version(src, version)
         return ev
 
 
@@ -343,15 +353,26 @@ class _DeviceEntry(_TensorEntry):
         self.cur_w = 0
         self.rows = RowRefs()        # SlabRows handed out by reserve()
         self.copy_event = None       # last host DMA into the slab (copy stream)
+        self.staging: List[Future] = []  # ingest-worker puts not yet checked
         self.last_flush_event = None  # last reduction reading the slab (compute stream)
         self.wait_before_copy = None
 
     # -- ring management -----------------------------------------------------
     def _copies_issued(self) -> None:
         """Host rows still being staged by the ingest worker have been issued
-        on its copy stream (copy_event is then their event)."""
+        on its copy stream (copy_event is then their event).  Every pending
+        put is checked, not only the last: the first failure (a tensor
+        modified in place, an allocation or HIP error) is raised here, so a
+        row that was never written cannot reach a reduction."""
+        if self.staging:
+            futs, self.staging = self.staging, []
+            _wait_futures(futs)
+            for f in futs:
+                if f.exception() is not None:
+                    self.copy_event = None
+                    raise f.exception()
         if isinstance(self.copy_event, Future):
-            self.copy_event = self.copy_event.result()  # raises a modified-tensor error
+            self.copy_event = self.copy_event.result()
 
     def _alloc(self, rows: int) -> None:
         self._copies_issued()
@@ -463,6 +484,7 @@ class _DeviceEntry(_TensorEntry):
             # the next client trains
             self.copy_event = self.agg._ingest(self.dev).put_async(
                 src, self.slab, r, wait_event=self.wait_before_copy)
+            self.staging.append(self.copy_event)
             self.wait_before_copy = None
         else:
             self.copy_event = self.agg._ingest(self.dev).put(

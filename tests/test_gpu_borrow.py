@@ -467,6 +467,36 @@ def test_handed_over_host_row_mutated_in_place_raises(dev):
         agg.pop("p")
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_earlier_handed_over_row_failure_is_not_lost(dev, pinned):
+    """Two handed-over host rows staged by the worker; the FIRST is changed
+    in place before its copy.  The later row's put succeeds, but the round
+    must still refuse: every pending put is checked at the reduction, not
+    only the newest (pageable sources: memmove into staging; pinned ones:
+    DMA'd straight from the caller's buffer)."""
+    import threading
+
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _ingest_for
+
+    agg = SerialAggregator(borrow=True, borrow_host=True)
+    gate = threading.Event()
+    _ingest_for(dev).pool.submit(gate.wait)  # the worker is busy until released
+    a, b = torch.ones(1 << 20), torch.full((1 << 20,), 2.0)
+    if pinned:
+        a, b = a.pin_memory(), b.pin_memory()
+    agg.add("p", a, 1)
+    agg.add("p", b, 1)
+    a.mul_(3)
+    gate.set()
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.pop("p")
+    # the next round's aggregator is unaffected
+    agg = SerialAggregator(borrow=True, borrow_host=True)
+    agg.add("q", b, 1)
+    assert torch.equal(agg.pop("q"), b)
+
+
 def test_host_client_keeping_its_vector_is_cloned(dev):
     """serial_aggregation under the borrowing aggregator: a host vector the
     client still references is cloned (the reference's snapshot), so changing

@@ -400,6 +400,11 @@ def test_changed_client_storage_keys():
     st.write("last_round", 3)
     st.write("new", 5)
     assert sorted(_changed_keys(st, state)) == ["d", "h", "last_round", "new"]
+    from fedsim_amd.distributed.centralized.centralized_fl_algorithm import _removed_keys
+
+    assert _removed_keys(st, state) == []
+    st.remove("same")
+    assert _removed_keys(st, state) == ["same"]
 
 
 def test_host_state_step_selection():

@@ -506,6 +506,12 @@ def _client_extras_worker(rank, world, port, outdir):
         def stateful(id, rounds, storage, *a, _f=synth.send_to_server, **k):
             n = storage.read("count") or 0
             storage.write("count", n + 1)
+            # an entry written on odd visits and removed on even ones
+            # (Storage.remove must reach the other ranks too)
+            if storage.read("flag") is not None:
+                storage.remove("flag")
+            else:
+                storage.write("flag", torch.tensor([float(id)]))
             storage.write("seen_rounds", torch.cat([storage.read("seen_rounds"),
                                                     torch.tensor([float(rounds)])])
                           if n else torch.tensor([float(rounds)]))
@@ -522,6 +528,8 @@ def _client_extras_worker(rank, world, port, outdir):
                              if alg._client_memory[cid].read("seen_rounds") is not None else [])
                        for cid in range(S.NUM_CLIENTS)}
         res["sampled"] = sampled
+        res["flag"] = {cid: alg._client_memory[cid].read("flag") is not None
+                       for cid in range(S.NUM_CLIENTS)}
 
         # (2) a diverged client in the third round: every rank stops there
         def diverging(id, rounds, *a, _f=synth.send_to_server, **k):
@@ -614,6 +622,16 @@ def _client_extras_worker(rank, world, port, outdir):
         except RuntimeError as e:
             res["drained"] = str(e)[:60]
 
+        # (7b) the same for the weight-1 row sums (FedDF's teacher targets)
+        agg = ClientShardedSerialAggregator(
+            entry_factory=DrainedChainEntry if rank == 1 else ChainOracleEntry,
+            step_impl=oracle_step)
+        try:
+            agg.ordered_rows_sum(torch.ones(2, 5) * (rank + 1), [0, 1], 5)
+            res["rows_drained"] = "ran"
+        except RuntimeError as e:
+            res["rows_drained"] = str(e)[:60]
+
         # (8) stateful clients and a divergence: clients after the diverged
         # one keep the storage they had before that round (the reference
         # never trained them)
@@ -663,10 +681,12 @@ def test_client_sharded_state_divergence_and_refusal():
         times = [i for i, s in enumerate(sampled) if cid in s]
         assert res[0]["count"][str(cid)] == len(times)
         assert res[0]["seen"][str(cid)] == [float(i) for i in times]
+        assert res[0]["flag"][str(cid)] == (len(times) % 2 == 1)
     assert res[0]["diverged_rounds"] == 2  # rounds 0 and 1 completed
     assert "depend on each other" in res[0]["adabest"], res[0]["adabest"]
     assert res[0]["desync"].startswith("the ranks of a client-sharded round sampled"), res[0]
     assert res[0]["drained"].startswith("client_reduction='chain': a rank drained"), res[0]
+    assert res[0]["rows_drained"] == res[0]["drained"], res[0]
     # round 2 trained its clients up to the diverged one (position 1)
     want = {cid: len([i for i, s in enumerate(sampled) if cid in s and
                       (i < 2 or (i == 2 and s.index(cid) <= 1))]) for cid in range(20)}
