@@ -21,6 +21,7 @@ from torch.utils.data import DataLoader
 
 from ... import scores as _scores
 from ...utils import AppendixAggregator, SerialAggregator, Storage, apply_on_dict
+from ...utils.handover import handover_round
 from ...utils.slab_rows import round_aggregator
 
 try:  # progress bar is cosmetic
@@ -361,7 +362,7 @@ class CentralFLAlgorithm(object):
             round_appendix_aggregator = AppendixAggregator()
             # clients that train on the GPU vectorize straight into this
             # round's HBM slab (utils/slab_rows.py)
-            with round_aggregator(round_serial_aggregator):
+            with round_aggregator(round_serial_aggregator), handover_round():
                 if hasattr(round_serial_aggregator, "client_block"):
                     diverged = self._client_sharded_round(round_serial_aggregator,
                                                           round_appendix_aggregator)

@@ -27,6 +27,7 @@ from torch.utils.data import DataLoader, RandomSampler
 
 from ....local import default_step_closure, local_inference, local_train
 from ....utils import vector_to_parameters_like, vectorize_module
+from ....utils.handover import hand_over
 from ....utils.slab_rows import reserve_round_row
 
 
@@ -77,9 +78,10 @@ def sgd_update(rounds, datasets, train_split_name, scores, epochs, criterion, tr
             model, DataLoader(split, batch_size=inference_batch_size, shuffle=False),
             scores[name], device=device)
         metrics[name] = _split_scores(scores, name)
-    # on the GPU the update is written straight into the round's HBM slab
+    # on the GPU the update is written straight into the round's HBM slab;
+    # the vector is fresh and kept nowhere: handed over to the server
     row = reserve_round_row("local_params", model)
-    return dict(local_params=vectorize_module(model, out=row), num_steps=n_steps,
+    return dict(local_params=hand_over(vectorize_module(model, out=row)), num_steps=n_steps,
                 diverged=diverged, num_samples=counts, metrics=metrics)
 
 

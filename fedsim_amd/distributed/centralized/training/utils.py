@@ -8,14 +8,15 @@ The reference's defensive ``clone()`` (utils.py:34) is kept only where it
 changes anything.  ``SerialAggregator.add`` snapshots host vectors (into the
 pinned staging ring) and, by default, HBM vectors (into the ring slab); the
 round driver's aggregator instead *borrows* HBM-resident vectors and reads
-them when the round is reduced.  Borrowing is only sound when the message held
-the sole reference to a tensor that shares its storage with nothing else (a
-fresh ``vectorize_module`` result): a client that reuses one output buffer, or
-keeps the tensor or a view of it, could otherwise change it before the round
-is reduced.  So the vector is cloned here -- the reference's own copy --
-whenever the aggregator would borrow it and that ownership cannot be shown
-(``_handed_over``); borrowing a tensor that is then modified in place anyway is
-caught by its version counter at the drain.
+them when the round is reduced.  Borrowing is only sound when the client gave
+the vector away: a client that reuses one output buffer, or keeps the tensor
+or a view of it, could otherwise change it before the round is reduced.  In
+the round driver that is declared, not inferred: the producer's hand-over
+token (utils/handover.py; the library's clients set it, local_updates.py)
+plus no alias of the storage.  The vector is cloned here -- the reference's
+own copy -- whenever the aggregator would borrow it and that ownership is not
+shown (``_handed_over``); a tensor modified in place after all is caught by
+its version counter at the drain.
 
 ``fused_server_step`` runs the FedAvg / AdaBest / FedDyn ``optimize`` epilogues
 (fedavg.py:193-208, adabest.py:172-189, feddyn.py:169-194) together with the
@@ -37,7 +38,7 @@ from .... import ops
 from ....local import local_inference
 from ....utils import initialize_module, vectorize_module
 from ....utils.aggregators import SerialAggregator as _DeviceSerialAggregator
-from ....utils.slab_rows import SlabRow
+from ....utils.handover import take_token, unaliased
 
 
 def serial_aggregation(
@@ -100,23 +101,19 @@ _OWNED_REFS = _owned_refs()
 
 
 def _handed_over(t: torch.Tensor) -> bool:
-    """Whether the client message holds the only reference to ``t`` and no
-    other tensor (view, base, alias) shares its storage.  Called with
+    """Whether ``t`` was given away by its client, so the aggregator may read
+    it after add returns.  Inside the round driver: an explicit hand-over
+    token (utils/handover.py) and no alias of its storage -- no reference
+    counting.  Outside it (receive_from_client called by user code): the
+    secondary guard, the message holding the only reference to ``t``
+    (calibrated reference count, _owned_refs) and no alias.  Called with
     serial_aggregation's ``params`` local, as _owned_refs measures."""
-    if not isinstance(t, torch.Tensor) or t._base is not None:
+    token = take_token(t)
+    if token is not None:
+        return token and unaliased(t)
+    if not isinstance(t, torch.Tensor) or _refcount(t) > _OWNED_REFS:
         return False
-    if _refcount(t) > _OWNED_REFS:
-        return False
-    if isinstance(t, SlabRow):
-        if t.in_slab:  # a reserved slab row: no storage of its own
-            return True
-        # read back already: torch ops on it may have handed out views of
-        # its copy, which add would then borrow
-        t = t._dense
-        if t is None:
-            return False
-    # one TensorImpl + the temporary storage object created here
-    return torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= 2
+    return unaliased(t)
 
 
 def _would_borrow(aggregator, t) -> bool:

@@ -9,6 +9,8 @@
 * parameter packing (``vectorize_module`` ...) — flat fp32 vectors and views.
 * ``set_seed`` / ``get_from_module`` — the reference's seeding and lookup
   helpers.
+* ``hand_over`` — a client's declaration that it gives its vector away (the
+  round driver's aggregator may then read it in place, handover.py).
 """
 from .aggregators import AppendixAggregator, DeviceAggregator, SerialAggregator
 from .convert_parameters import (
@@ -19,6 +21,7 @@ from .convert_parameters import (
     vectorize_module_grads,
 )
 from .dict_ops import apply_on_dict
+from .handover import hand_over
 from .misc import get_from_module, set_seed
 from .storage import Storage
 
@@ -26,4 +29,5 @@ __all__ = [
     "SerialAggregator", "DeviceAggregator", "AppendixAggregator", "Storage", "apply_on_dict",
     "vectorize_module", "vectorize_module_grads", "initialize_module",
     "vector_to_parameters_like", "vector_to_named_parameters_like", "get_from_module", "set_seed",
+    "hand_over",
 ]

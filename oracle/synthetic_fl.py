@@ -15,6 +15,8 @@ from torch import nn
 from torch.nn.utils import parameters_to_vector
 from torch.utils.data import TensorDataset
 
+from fedsim_amd.utils.handover import hand_over
+
 from . import vectors as V
 
 NUM_CLIENTS = 20
@@ -103,8 +105,10 @@ def synthetic_send_to_server(id, rounds, storage, datasets, train_split_name, sc
     delta = torch.from_numpy((0.01 * V.gauss(id * 7919 + rounds, base.numel())).astype(np.float32))
     local = base + delta.to(base.dtype)  # the model's dtype (a no-op for fp32 models)
     n = len(datasets[train_split_name])
+    # a fresh vector the client keeps nowhere: declared handed over (the
+    # round driver's aggregator may read it in place, fedsim_amd handover.py)
     return dict(
-        local_params=local.to(device),
+        local_params=hand_over(local.to(device)),
         num_steps=max(1, n // 32),
         diverged=False,
         num_samples={train_split_name: n},

@@ -431,3 +431,58 @@ def test_async_host_staging_threshold():
     from fedsim_amd.utils.aggregators import _ASYNC_STAGE_MIN
 
     assert 199_210 < _ASYNC_STAGE_MIN <= 1_085_668
+
+
+def test_hand_over_tokens_decide_borrowing_in_the_driver(monkeypatch):
+    """Inside a driver round, serial_aggregation's ownership test is the
+    explicit hand-over token plus the no-alias check -- the reference count
+    is never consulted; outside one, the reference-count guard applies."""
+    from fedsim_amd.distributed.centralized.training import utils as U
+    from fedsim_amd.utils.handover import hand_over, handover_round
+
+    def no_refcount(t):
+        raise AssertionError("the driver's borrow decision must not count references")
+
+    with handover_round():
+        monkeypatch.setattr(U, "_refcount", no_refcount)
+        fresh = hand_over(torch.ones(8))
+        assert U._handed_over(fresh)
+        assert not U._handed_over(fresh)  # a token is consumed once
+        assert not U._handed_over(torch.ones(8))  # no declaration: the clone
+        kept = hand_over(torch.ones(8))
+        view = kept[:4]  # noqa: F841 -- the client keeps a view of its output
+        assert not U._handed_over(kept)
+        changed = hand_over(torch.ones(8))
+        changed.add_(1)  # changed after it was handed over
+        assert not U._handed_over(changed)
+        sliced = torch.ones(16)
+        part = hand_over(sliced[:8])  # itself a view of another tensor
+        assert not U._handed_over(part)
+        again = hand_over(torch.ones(8))
+        assert U._handed_over(again)
+        alias = hand_over(again.detach())  # the same storage a second time
+        assert not U._handed_over(alias)
+        monkeypatch.undo()
+    # outside a round: hand_over is a no-op and the reference count decides
+    msg = {"local_params": hand_over(torch.ones(8))}
+    params = msg["local_params"]
+    assert U._handed_over(params)  # the message holds the only reference
+    kept = params  # noqa: F841 -- the client keeps it
+    assert not U._handed_over(params)
+
+
+def test_hand_over_round_scope_releases_tokens():
+    import gc
+    import weakref
+
+    from fedsim_amd.utils.handover import _OPEN, hand_over, handover_round, take_token
+
+    with handover_round():
+        t = hand_over(torch.ones(4))
+        ref = weakref.ref(t)
+        del t
+        gc.collect()
+        assert ref() is None  # a token does not keep its tensor alive
+        u = torch.ones(4)
+        assert take_token(u) is False
+    assert not _OPEN and take_token(u) is None
