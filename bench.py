@@ -85,6 +85,10 @@ def parse(argv=None):
     ap.add_argument("--no-epilogue", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-selftest", action="store_true",
+                    help="skip the multi-GPU self-test that precedes the timed region")
+    ap.add_argument("--selftest-fault-rank", type=int, default=None,
+                    help="TEST ONLY: flip one result bit on this rank in the self-test")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--master-port", type=int, default=0,
                     help="rendezvous port of the self-spawned ranks (0: pick a free one)")
@@ -439,6 +443,185 @@ def cpu_baseline(P, budget_s):
     )
 
 
+# -- multi-GPU self-test (outside the timed region) -------------------------
+SELFTEST_K, SELFTEST_P = 24, 20_011  # ~2 MB of client rows: seconds, not minutes
+
+
+def _oracle_reduce(X, w32, out, acc_in, W):
+    """Rehearsal stand-in for a rank's HIP reduction: the C oracle (bitwise
+    the reference), so the rehearsal checks the protocol, not arithmetic."""
+    import numpy as np
+    import torch
+
+    from oracle import ref
+
+    ai = None if acc_in is None else np.ascontiguousarray(acc_in.numpy()).copy()
+    res = ref.reduce(np.ascontiguousarray(X.numpy()), [float(v) for v in w32.tolist()],
+                     acc_in=ai, W=W)
+    out.copy_(torch.from_numpy(res))
+    return out
+
+
+def _oracle_step(step, avg):
+    """Rehearsal stand-in for the HIP server step: the C oracle's."""
+    from oracle import ref
+
+    avg = avg.contiguous()
+    a, g = step.args, step.sgd
+    ref.lib().ref_server_step_f32(a.algo, avg.data_ptr(), a.coef, a.cloud, a.aux, a.avg_prev,
+                                  a.momentum_buf, a.momentum_init, a.grad_out, g.neg_lr,
+                                  g.momentum, g.one_minus_dampening, g.weight_decay, g.nesterov,
+                                  g.maximize, step.P)
+
+
+def _rehearsal_entry():
+    """entry_factory of the aggregators in the CPU rehearsal: a rank's rows
+    reduced by the C oracle (onto another rank's running sum for the chain)."""
+    import torch
+
+    from fedsim_amd import ops
+    from fedsim_amd.utils.aggregators import _TensorEntry
+
+    class Entry(_TensorEntry):
+        def __init__(self, part, agg):
+            self.P, self.dev, self.rows, self.ws, self.cur_w = part.numel(), part.device, [], [], 0
+
+        def add(self, value, weight):
+            new_w = self.cur_w + weight
+            self.rows.append(value.detach().reshape(-1).clone())
+            self.ws.append(weight)
+            self.cur_w = new_w
+
+        def partial(self, acc_in, W=None):
+            out = torch.empty(self.P)
+            w32 = torch.tensor([ops.fl32(w) for w in self.ws])
+            return _oracle_reduce(torch.stack(self.rows), w32, out, acc_in, W)
+
+        def get(self):
+            return self.partial(None, self.cur_w if self.cur_w else None)
+
+        def get_sum(self):
+            return self.partial(None)
+
+        def pop(self, on_device=False):
+            return self.get()
+
+        def pop_step(self, step):
+            _oracle_step(step, self.get())
+
+        def chainable(self):
+            return True
+
+    return Entry
+
+
+def multi_gpu_selftest(rk, fault_rank=None):
+    """One small round through every multi-GPU path over the job's real
+    process group (RCCL on the GPUs; gloo in the rehearsal), each checked
+    against the C oracle (oracle/ref.py) on every column: SURVEY §8e's
+    decompositions of aggregators.py:23-40,104-122.
+
+      sharded_pop_step    ShardedSerialAggregator: column shards, server step
+                          on each, one all-gather of the operands   bitwise
+      client_chain        ClientShardedSerialAggregator(mode="chain"): the
+                          running sum passed rank to rank + broadcast  bitwise
+      client_allreduce    mode="allreduce": partial sums + RCCL all-reduce
+                          (reordered)                        normwise <= 1e-6
+      param_sharded_step  sharding.param_sharded_step on this rank's column
+                          shard (blocked slab, fused step)           bitwise
+
+    Every rank checks its own result; the verdicts are combined with a MIN
+    all-reduce, so every rank agrees.  Returns the dict that goes into the
+    line as ``multi_gpu_selftest``."""
+    import numpy as np
+    import torch
+
+    from fedsim_amd import ops, sharding
+    from fedsim_amd.sharding import (ClientShardedSerialAggregator, RemoteRow,
+                                     ShardedSerialAggregator)
+    from oracle import ref
+    from oracle import vectors as V
+
+    t0 = time.perf_counter()
+    K, P, world, me, dev = SELFTEST_K, SELFTEST_P, rk.world, rk.rank, rk.dev
+    X = V.client_rows("realistic", K, P, 17)  # the same on every rank
+    w = V.client_weights("fedavg", K, 17)
+    W = sum(w)
+    avg_ref = ref.reduce(X, w, W=W)
+    cloud0 = V.cloud_vector(P, 18)
+    cloud_ref = ref.fedavg_sgd(avg_ref, cloud0, 1.0)
+    grad_ref = (cloud0 - avg_ref).astype(np.float32)
+    entry = _rehearsal_entry() if rk.rehearsal else None
+    kw = dict(entry_factory=entry) if entry is not None else {}
+    checks = {}
+
+    def record(name, got, want, bitwise=True):
+        got = np.ascontiguousarray(got, dtype=np.float32)
+        if bitwise:
+            bad = int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))
+            checks[name] = dict(bitwise=True, columns=int(want.size), mismatched=bad, ok=bad == 0)
+        else:
+            err = float(np.linalg.norm(got.astype(np.float64) - want) / np.linalg.norm(want))
+            checks[name] = dict(bitwise=False, columns=int(want.size), rel_err=err,
+                                tol=1e-6, ok=err <= 1e-6)
+
+    def row(k):
+        return torch.from_numpy(X[k].copy()).to(dev)
+
+    # (1) parameter-sharded aggregator: pop + server step, all-gather
+    agg = ShardedSerialAggregator(**kw)
+    for k in range(K):
+        agg.add("p", row(k), w[k])
+    cloud = torch.from_numpy(cloud0.copy()).to(dev)
+    grad = torch.empty_like(cloud)
+    agg.pop_step("p", ops.ServerStep("fedavg", cloud, lr=1.0, grad_out=grad))
+    record("sharded_pop_step", cloud.cpu().numpy(), cloud_ref)
+    record("sharded_pop_step_grad", grad.cpu().numpy(), grad_ref)
+    # (2) client-sharded: each rank holds one contiguous block of the clients
+    spans = [sharding.shard_range(K, r, world) for r in range(world)]
+    owner = [next(r for r, (lo, hi) in enumerate(spans) if lo <= k < hi) for k in range(K)]
+    for mode in ("chain", "allreduce"):
+        agg = ClientShardedSerialAggregator(mode=mode, **kw,
+                                            **(dict(step_impl=_oracle_step) if entry else {}))
+        for k in range(K):
+            v = row(k) if owner[k] == me else RemoteRow(
+                (P,), torch.float32, "cpu" if rk.rehearsal else "cuda", owner[k])
+            agg.add("p", v, w[k])
+        record("client_" + mode, agg.pop("p").cpu().numpy(), avg_ref, bitwise=mode == "chain")
+    # (3) the parameter-sharded round step of bench's own headline mode
+    lo, hi = sharding.shard_range(P, me, world, sharding.ALIGN)
+    w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)
+    cloud = torch.from_numpy(cloud0.copy()).to(dev)
+    step = ops.ServerStep("fedavg", cloud, lr=1.0).narrow(lo, hi)
+    if hi > lo:
+        Xs = torch.from_numpy(np.ascontiguousarray(X[:, lo:hi])).to(dev)
+        if rk.rehearsal:
+            avg = sharding.param_sharded(Xs, w32, W, torch.empty(hi - lo),
+                                         local_reduce=lambda *args: _oracle_reduce(*args[:5]))
+            _oracle_step(step, avg)
+        else:
+            C = ops.choose_block_cols(hi - lo)
+            sharding.param_sharded_step(ops.to_blocked(Xs, C), w32, W, step)
+    got = cloud[lo:hi].cpu().numpy()
+    if fault_rank == me:  # TEST ONLY: a wrong bit on one rank must fail every rank
+        got = got.copy()
+        got.view(np.uint32)[:1] ^= 1
+    record("param_sharded_step", got, cloud_ref[lo:hi])
+    ok = all(c["ok"] for c in checks.values())
+    if rk.dist is not None:  # every rank's verdict, agreed by all
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                         device="cpu" if rk.dist.get_backend() == "gloo" else dev)
+        rk.dist.all_reduce(t, op=rk.dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    if not rk.rehearsal:
+        torch.cuda.synchronize()
+    return dict(ok=ok, agreed="MIN of every rank's verdict (all-reduce)" if rk.dist else None,
+                world=world, backend=rk.dist.get_backend() if rk.dist else None,
+                K=K, P=P, seconds=round(time.perf_counter() - t0, 3),
+                checker="oracle/ref.py (C restatement, pinned to the reference's goldens)",
+                checks=checks)
+
+
 def fedavg_step(rk, P):
     """FedAvg.optimize's server step operands (default SGD lr 1.0,
     fed_learn.py:129; cloud.grad = pseudo-gradient as torch leaves it)."""
@@ -648,6 +831,7 @@ def _main(a, quiet):
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={rk.world}")
     clock = KernelClock(rk)
     ar_ms = []
+    selftest = None if a.no_selftest else multi_gpu_selftest(rk, a.selftest_fault_rank)
     if a.mode == "param":
         step, info, total_bytes, keep = setup_param(a, rk, clock)
     else:
@@ -694,6 +878,7 @@ def _main(a, quiet):
                  "cyclically; FedAvg int weights U{50..600})"),
         "config": dict(info, mode_flag=a.mode),
     }
+    result["multi_gpu_selftest"] = selftest
     result["world_size_seen"] = rk.dist.get_world_size() if rk.dist is not None else 1
     result["backend"] = rk.dist.get_backend() if rk.dist is not None else None
     if rk.rehearsal:
@@ -735,6 +920,9 @@ def _main(a, quiet):
     if rk.dist is not None:
         rk.dist.barrier()
         rk.dist.destroy_process_group()
+    if selftest is not None and not selftest["ok"]:
+        sys.stderr.write("bench: multi-GPU self-test FAILED: %s\n" % json.dumps(selftest))
+        sys.exit(3)
 
 
 if __name__ == "__main__":

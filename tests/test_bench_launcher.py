@@ -40,6 +40,36 @@ def test_launcher_one_line(mode, gpus):
     if mode == "allreduce":
         assert d["config"]["clients_K"] == 9 * gpus
     assert d["value"] > 0
+    _selftest_ok(d, gpus)
+
+
+SELFTEST_CHECKS = {"sharded_pop_step", "sharded_pop_step_grad", "client_chain",
+                   "client_allreduce", "param_sharded_step"}
+
+
+def _selftest_ok(d, world):
+    """The line carries the multi-GPU self-test: every path checked against
+    the oracle over the job's process group, agreed by every rank."""
+    st = d["multi_gpu_selftest"]
+    assert st["ok"] and st["world"] == world, st
+    assert set(st["checks"]) == SELFTEST_CHECKS
+    for name, c in st["checks"].items():
+        assert c["ok"], (name, c)
+        assert c["bitwise"] == (name != "client_allreduce")
+
+
+def test_selftest_mismatch_fails_every_rank():
+    """A wrong bit on one rank's shard: every rank agrees the self-test
+    failed, the line says so, and the run exits non-zero."""
+    r = _bench("--gpus", "3", "--rehearsal-stub", "tests.bench_stub:reduce", "--K", "4",
+               "--P", "256", "--steps", "1", "--warmup", "1", "--selftest-fault-rank", "2",
+               timeout=180)
+    assert r.returncode == 3, r.stderr[-2000:]
+    assert "multi-GPU self-test FAILED" in r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    st = json.loads(lines[0])["multi_gpu_selftest"]
+    assert st["ok"] is False and st["checks"]["param_sharded_step"]["ok"] is True  # rank 0's
 
 
 def test_launcher_rank_failure_fails_run():
@@ -97,3 +127,4 @@ def test_driver_command_at_8_ranks(mode):
     if mode == "strong":
         assert d["config"]["params_total"] == 1000
     assert "cpu_baseline" not in d or d["cpu_baseline"] is None  # rank 0 at N=1 only
+    _selftest_ok(d, 8)

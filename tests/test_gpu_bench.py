@@ -35,3 +35,41 @@ def test_launcher_two_ranks_one_gpu(mode, extra):
     assert "rehearsal" in d
     if mode == "allreduce":
         assert d["allreduce"]["ms"] is not None
+    _selftest_ok(d, 2, "gloo")
+
+
+def _selftest_ok(d, world, backend):
+    from test_bench_launcher import SELFTEST_CHECKS
+
+    st = d["multi_gpu_selftest"]
+    assert st["ok"] and st["world"] == world and st["backend"] == backend, st
+    assert set(st["checks"]) == SELFTEST_CHECKS and all(c["ok"] for c in st["checks"].values())
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("launch", ["plain", "torchrun_rccl"])
+def test_one_gpu_line_carries_selftest(launch):
+    """N=1 as the driver runs it (plain) and under torch.distributed.run
+    with one rank (the RCCL process-group path): the HIP aggregators'
+    multi-GPU paths checked against the oracle before the timed region."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    args = [os.path.join(REPO, "bench.py"), "--gpus", "1", "--K", "64", "--P", "2000000",
+            "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    if launch == "torchrun_rccl":
+        args = ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
+    r = subprocess.run([sys.executable, *args], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    _selftest_ok(d, 1, "nccl" if launch == "torchrun_rccl" else None)
