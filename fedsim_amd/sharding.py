@@ -848,8 +848,10 @@ class ClientShardedSerialAggregator(SerialAggregator):
         if self.mode == "chain":
             # a chained partial continues the previous rank's sum, so no row
             # may be drained from +0 before it: hold every borrowed row (the
-            # round's local messages are all alive until received anyway)
+            # round's local messages are all alive until received anyway),
+            # and grow the ring of snapshotted rows instead of draining it
             e.Bmax = 1 << 62
+            e.keep_pending = True
         return e
 
     # -- collectives shared by the tensor keys and FedDF's teacher targets --

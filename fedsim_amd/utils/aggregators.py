@@ -338,6 +338,8 @@ class _DeviceEntry(_TensorEntry):
         self.Bmax = max(1, min(opts.max_rows, budget // max(4, 4 * self.P)))
         self.borrowed: List = []
         self.borrowed_ptrs: List[int] = []  # their data pointers (the row table)
+        # grow the ring without draining it (chained partial sums, _grow)
+        self.keep_pending = False
         self.R = 0
         self.slab: Optional[torch.Tensor] = None
         self.hint = opts.expected_rows
@@ -385,6 +387,30 @@ class _DeviceEntry(_TensorEntry):
         # host DMA into the new slab waits for the latest one
         self.wait_before_copy = self.last_flush_event
 
+    def _grow(self, rows: int) -> None:
+        """A larger ring that keeps the pending rows, in arrival order, as its
+        first rows (two D2D copies on the compute stream) instead of draining
+        them: a chained partial sum (client-sharded rounds) must see every row
+        of this rank still pending when the chain reaches it."""
+        self._copies_issued()
+        cur = torch.cuda.current_stream(self.dev)
+        if self.copy_event is not None:
+            cur.wait_event(self.copy_event)
+            self.copy_event = None
+        old, n, t = self.slab, self.n_pending, self.tail
+        new = torch.empty((self.nblk, rows, self.C), dtype=torch.float32, device=self.dev)
+        first = min(n, self.R - t)
+        new[:, :first].copy_(old[:, t:t + first])
+        if n > first:
+            new[:, first:n].copy_(old[:, :n - first])
+        self.rows.release(old)
+        self.slab, self.R, self.tail, self.head = new, rows, 0, n % rows
+        # host DMAs into the new ring (copy stream) start after everything the
+        # compute stream has queued: its block may be recycled memory
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self.wait_before_copy = ev
+
     def _make_room(self) -> None:
         if self.slab is None:
             first = self.hint if self.hint else 8
@@ -392,6 +418,9 @@ class _DeviceEntry(_TensorEntry):
             return
         if self.R < self.Rmax:
             if self.n_pending == self.R:
+                if self.keep_pending:
+                    self._grow(min(self.Rmax, 2 * self.R))
+                    return
                 self._flush(final_W=None)
                 self._alloc(min(self.Rmax, 2 * self.R))
         elif self.n_pending >= max(1, self.Rmax // 2):

@@ -524,3 +524,30 @@ def test_client_sharded_feddf_two_ranks_on_one_gpu(mode):
             for r in rep:
                 assert r["replayed"] and r["fallbacks"] == 0 and r["conv_launches"] > 0, r
             assert sum(r["teachers_local"] for r in rep) == 4
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_chained_entry_grows_without_draining(where):
+    """A client-sharded rank's snapshotted rows (borrow off, host or HBM
+    sources) through several ring growths: the chain entry grows its ring by
+    copying the pending rows instead of draining them from +0, so it can
+    still continue another rank's running sum -- bitwise the oracle's
+    arrival-order sum from that acc_in."""
+    from fedsim_amd.sharding import ClientShardedSerialAggregator
+
+    dev = torch.device("cuda:0")
+    K, P = 37, 50_003
+    X = V.client_rows("realistic", K, P, 31)
+    w = V.client_weights("fedavg", K, 31)
+    acc0 = V.cloud_vector(P, 32)
+    agg = ClientShardedSerialAggregator(mode="chain")
+    e = agg._local_entry("p", torch.empty(P, device=dev))
+    assert e.keep_pending and e.Rmax > K
+    for k in range(K):
+        src = torch.from_numpy(X[k].copy())
+        e.add(src if where == "host" else src.to(dev), w[k])
+        src.fill_(float("nan"))  # snapshotted at add
+    assert e.R >= K and e.acc is None and e.chainable()
+    got = e.partial(torch.from_numpy(acc0.copy()).to(dev), W=sum(w))
+    want = ref.reduce(X, w, acc_in=acc0.copy(), W=sum(w))
+    np.testing.assert_array_equal(bits(got.cpu().numpy()), bits(want))
