@@ -2109,14 +2109,7 @@ __device__ __forceinline__ float pool_dpp_max(float m) {
   return (v > m || __builtin_isnan(v)) ? v : m;
 }
 
-// WPC / CPC (0: runtime): the padded row pitch Wp and the staged channel
-// pitch nrows * Wp as compile-time constants for the reference models' first
-// convs (conv_flat_geometry): every k step's LDS operand read is then a
-// per-lane base plus an immediate offset.  The two lanes of a k pair differ
-// by the step from tap r to r + 1 -- one column, one row wrap, or one channel
-// wrap, three compile-time distances -- so each lane keeps three bases and a
-// step picks one at compile time: no address arithmetic in the k loop.
-template <int KS, int CI, int XM, bool HALF, bool POOL, int WPC = 0, int CPC = 0>
+template <int KS, int CI, int XM, bool HALF, bool POOL>
 __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_teacher_conv2d_flat(
     const float* __restrict__ x, int64_t x_kstride, const float* __restrict__ params,
     int64_t params_kstride, int64_t w_off, int64_t b_off, fedagg_conv2d_shape s, int nslot,
@@ -2147,7 +2140,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(5,
   const int H = static_cast<int>(s.H), W = static_cast<int>(s.W);
   const int OW = static_cast<int>(s.OW);
   const int OHW = static_cast<int>(s.OH * s.OW);
-  const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = WPC ? WPC : OW + KS - 1;
+  const int Hp = static_cast<int>(s.OH) + KS - 1, Wp = OW + KS - 1;
   const int HW = H * W;
   const int OH = static_cast<int>(s.OH);
   // pooled planes (POOL): PH x PW windows of 2 x 2, four pixel slots each
@@ -2176,7 +2169,7 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(5,
   // + row, from g = row_lo on: sX[c][g - row_lo][col], ``nrows`` rows per
   // channel (the host's bound for any tile), so the workgroup's LDS holds
   // only those rows and more workgroups fit on a CU.
-  const int CP = CPC ? CPC : nrows * Wp;  // channel pitch in sX
+  const int CP = nrows * Wp;  // channel pitch in sX
   const int pend = (px0 + TPX < NPX ? px0 + TPX : NPX) - 1;
   // slot of the tile's last image; the padded rows its pixels read (POOL:
   // whole images, a window's rows straddle the tile's first / last row)
@@ -2306,33 +2299,16 @@ __global__ __launch_bounds__(kFlatThreads) __attribute__((amdgpu_waves_per_eu(5,
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-  // compile-time geometry: the k pair's second tap is its first + 1 column,
-  // + one row wrap (DROW) or + one channel wrap (DCH) away
-  constexpr int DROW = WPC - (KS - 1), DCH = CPC - (KS - 1) * WPC - (KS - 1);
-  int xbd[3][NPG];
-#pragma unroll
-  for (int b = 0; b < NPG; ++b) {
-    xbd[0][b] = xb[b] + kk;
-    xbd[1][b] = xb[b] + kk * DROW;
-    xbd[2][b] = xb[b] + kk * DCH;
-  }
 #pragma unroll
   for (int st = 0; st < RP; ++st) {
     const int r0 = 2 * st, r1 = 2 * st + 1;
     const int o0 = (r0 / TAPS) * CP + ((r0 % TAPS) / KS) * Wp + r0 % KS;
     const int o1 = r1 < R ? (r1 / TAPS) * CP + ((r1 % TAPS) / KS) * Wp + r1 % KS : 0;
+    const int ob = kk ? o1 : o0;
     const float a0 = pa[2 * st];
     float bv[NPG];
-    if constexpr (WPC > 0 && CPC > 0) {
-      const int d = r1 < R ? o1 - o0 : 0;  // compile-time: 1, DROW or DCH
-      const int j = d == DROW ? 1 : d == DCH && d != 1 ? 2 : 0;
 #pragma unroll
-      for (int b = 0; b < NPG; ++b) bv[b] = sX[xbd[j][b] + o0];
-    } else {
-      const int ob = kk ? o1 : o0;
-#pragma unroll
-      for (int b = 0; b < NPG; ++b) bv[b] = sX[xb[b] + ob];
-    }
+    for (int b = 0; b < NPG; ++b) bv[b] = sX[xb[b] + ob];
     if (r1 >= R && kk) {  // the zero term of an odd R
 #pragma unroll
       for (int b = 0; b < NPG; ++b) bv[b] = 0.f;
@@ -3094,230 +3070,6 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
   }
 }
 
-
-#ifdef FEDAGG_POOL_DMA
-// s_waitcnt vmcnt(n) for a runtime n (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4]
-// << 14, expcnt 7, lgkmcnt 15); n above 15 waits for 15 (stricter, safe).
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  switch (n < 15 ? n : 15) {
-#define FEDAGG_VM(i) case i: __builtin_amdgcn_s_waitcnt(0x0f70 | i); break;
-    FEDAGG_VM(0) FEDAGG_VM(1) FEDAGG_VM(2) FEDAGG_VM(3) FEDAGG_VM(4) FEDAGG_VM(5)
-    FEDAGG_VM(6) FEDAGG_VM(7) FEDAGG_VM(8) FEDAGG_VM(9) FEDAGG_VM(10) FEDAGG_VM(11)
-    FEDAGG_VM(12) FEDAGG_VM(13) FEDAGG_VM(14)
-#undef FEDAGG_VM
-    default: __builtin_amdgcn_s_waitcnt(0x0f7f); break;
-  }
-}
-
-// a workgroup barrier that leaves LDS-DMA loads in flight (no vmcnt(0): the
-// fence of __syncthreads() would drain them)
-__device__ __forceinline__ void barrier_lds_only() {
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
-  __builtin_amdgcn_s_barrier();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// k_pad_lrn_maxpool_slide with the raw channels staged through LDS by
-// LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction) instead
-// of register loads: a ring of RU units of CB channels each ([RU][CB][HW]
-// floats) holds the raw planes, units b and b + 1 are read by block b, and
-// up to RU - 2 further units are in flight while it is normalised and
-// pooled, so the bytes in flight are set by LDS, not by the VGPR budget.
-// The window still slides in registers; same arithmetic, element for
-// element (a raw value read from LDS is the value the register load read).
-// Needs HW % 4 == 0 (channel planes on 16-B boundaries: a channel outside
-// [0, C) is a whole run of out-of-range chunks, read as 0).
-template <int SIZE, int NQ, int CB, int RU>
-__global__ __launch_bounds__(256) void k_pad_lrn_maxpool_dma(const float* __restrict__ x,
-                                                             fedagg_pool_args a, int64_t CG,
-                                                             int64_t OH, int64_t OW,
-                                                             int64_t n_base,
-                                                             float* __restrict__ y) {
-  extern __shared__ float lds[];
-  constexpr int LO = SIZE > 0 ? SIZE / 2 : 0;
-  constexpr int SW = SIZE > 0 ? SIZE : 1;
-  constexpr int LEAD = SW - 1 - LO;
-  static_assert(LO + LEAD <= CB && CB % 4 == 0 && RU >= 3, "ring geometry");
-  const int64_t n = n_base + blockIdx.y;
-  const int C = static_cast<int>(a.C);
-  const int g0 = static_cast<int>(blockIdx.x * CG);
-  const int g1 = static_cast<int>(a.C - g0 < CG ? a.C : g0 + CG);
-  const int H = static_cast<int>(a.H), W = static_cast<int>(a.W);
-  const int Hp = H + static_cast<int>(a.pad_top + a.pad_bottom);
-  const int Wp = W + static_cast<int>(a.pad_left + a.pad_right);
-  const int HpWp = Hp * Wp;
-  const int HW = H * W;
-  const int OHW = static_cast<int>(OH * OW);
-  const float* xn = x + n * a.C * HW;
-  const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xn), static_cast<short>(0), static_cast<int>(a.C * HW * 4), 0x00020000);
-  const int unit = CB * HW;  // floats per ring unit
-  float* ring = lds;
-  float* plane = lds + RU * unit;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // unit u: channels [g0 - LO + CB u, + CB) (outside [0, C): zeros)
-  const int n16 = unit >> 2;             // 16-B chunks per unit
-  const int ninst = (n16 + 63) >> 6;     // wave-instructions per unit
-  const int M = (ninst + 3) >> 2;        // per wave (the last repeats its own)
-  const int last_unit = (g1 - 1 + LEAD - (g0 - LO)) / CB;
-  auto dma = [&](int u) {
-    float* dst = ring + (u % RU) * unit;
-    const int byte0 = (g0 - LO + CB * u) * HW * 4;
-    for (int j = 0; j < M; ++j) {
-      int i = 4 * j + wave;
-      if (i >= ninst) i = ninst - 1;  // every wave issues M: a uniform vmcnt
-      const int chunk = 64 * i + lane;
-      if (chunk < n16)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            xres, (__attribute__((address_space(3))) void*)(dst + 256 * i), 16,
-            byte0 + chunk * 16, 0, 0, 0);
-    }
-  };
-  int issued = 0;
-  for (; issued < RU && issued <= last_unit; ++issued) dma(issued);
-
-  bool in[NQ];
-  int roff[NQ];  // offset of each position in a raw channel plane
-#pragma unroll
-  for (int i = 0; i < NQ; ++i) {
-    const int q = threadIdx.x + 256 * i;
-    const int ph = q / Wp;
-    const int ih = ph - static_cast<int>(a.pad_top);
-    const int iw = q - ph * Wp - static_cast<int>(a.pad_left);
-    in[i] = q < HpWp && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
-            static_cast<unsigned>(iw) < static_cast<unsigned>(W);
-    roff[i] = in[i] ? ih * W + iw : 0;
-  }
-  constexpr int NM = (CB * NQ + 3) / 4;
-  const int pk = static_cast<int>(a.pool_kh);
-  const bool map = a.pool_kh == a.pool_kw && (pk == 2 || pk == 3) && CB * OHW <= 256 * NM;
-  const int bph = map ? static_cast<int>(a.pool_ph) : 0, bpw = map ? static_cast<int>(a.pool_pw) : 0;
-  const int WpE = Wp + 2 * bpw;
-  const int HpWpE = (Hp + 2 * bph) * WpE;
-  PoolStep ps;
-  {
-    const int sh = static_cast<int>(a.pool_sh), sw = static_cast<int>(a.pool_sw);
-    const int ow_n = static_cast<int>(OW), oh_n = static_cast<int>(OH);
-    const int e = threadIdx.x;
-    const int cc = e / OHW;
-    ps.oh = (e - cc * OHW) / ow_n;
-    ps.ow = e - cc * OHW - ps.oh * ow_n;
-    ps.src = cc * HpWpE + ps.oh * sh * WpE + ps.ow * sw;
-    const int dcc = 256 / OHW;
-    ps.d_oh = (256 - dcc * OHW) / ow_n;
-    ps.d_ow = 256 - dcc * OHW - ps.d_oh * ow_n;
-    ps.d_src = dcc * HpWpE + ps.d_oh * sh * WpE + ps.d_ow * sw;
-    ps.wrap_ow_src = sh * WpE - ow_n * sw;
-    ps.wrap_oh_src = HpWpE - oh_n * sh * WpE;
-    ps.OH = oh_n;
-    ps.OW = ow_n;
-  }
-  int wq[NQ];
-#pragma unroll
-  for (int i = 0; i < NQ; ++i) {
-    const int q = threadIdx.x + 256 * i;
-    const int ph = q / Wp;
-    wq[i] = (ph + bph) * WpE + (q - ph * Wp) + bpw;
-  }
-  if (bph | bpw) {
-    for (int e = threadIdx.x; e < CB * HpWpE; e += 256) plane[e] = -__builtin_inff();
-  }
-  // raw channel ch (relative index r = ch - (g0 - LO)) of every position
-  auto raw_at = [&](float (&dst)[NQ], int r) {
-    const float* src = ring + ((r / CB) % RU) * unit + (r % CB) * HW;
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) dst[i] = in[i] ? src[roff[i]] : 0.f;
-  };
-  constexpr bool RING = CB % SW == 0;
-  auto slot = [](int j, int t) { return RING ? (j + t) % SW : t; };
-  float win[SW][NQ];
-  float sq[SW][NQ];
-  const float size_f = static_cast<float>(a.lrn_size);
-  const float nbeta = -a.lrn_beta;
-  int b = 0;
-  for (int c0 = g0; c0 < g1; c0 += CB, ++b) {
-    const int cbn = g1 - c0 < CB ? g1 - c0 : CB;
-    // units b and b + 1 landed (every wave's share), later ones may fly
-    const int need = b + 1 < last_unit ? b + 1 : last_unit;
-    wait_vmcnt(M * (issued - 1 - need));
-    barrier_lds_only();
-    if (b == 0) {
-#pragma unroll
-      for (int t = 0; t + 1 < SW; ++t) {
-        const int u = RING ? t : t + 1;
-        raw_at(win[u], t);
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) sq[u][i] = win[u][i] * win[u][i];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < CB; ++j) {
-      if (j < cbn) {
-        if constexpr (!RING) {
-#pragma unroll
-          for (int t = 0; t + 1 < SW; ++t)
-#pragma unroll
-            for (int i = 0; i < NQ; ++i) {
-              win[t][i] = win[t + 1][i];
-              sq[t][i] = sq[t + 1][i];
-            }
-        }
-        float rv[NQ];
-        raw_at(rv, CB * b + LO + LEAD + j);
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-          win[slot(j, SW - 1)][i] = rv[i];
-          sq[slot(j, SW - 1)][i] = rv[i] * rv[i];
-        }
-        float vv[NQ];
-        float bb[NQ];
-        bool slow = false;
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-          vv[i] = win[slot(j, LO)][i];
-          if constexpr (SIZE > 0) {
-            float sum = sq[slot(j, 0)][i];
-#pragma unroll
-            for (int t = 1; t < SIZE; ++t) sum = sum + sq[slot(j, t)][i];
-            bb[i] = lrn_base<SIZE>(sum, size_f, a.lrn_alpha, a.lrn_k);
-            float r;
-            const bool fast = lrn_fast_scale(bb[i], nbeta, r);
-            slow = slow || (in[i] && !fast);
-            vv[i] = in[i] ? vv[i] * r : vv[i];
-          }
-        }
-        if constexpr (SIZE > 0) {
-          if (__builtin_expect(__ballot(slow) != 0, 0)) {
-#pragma unroll
-            for (int i = 0; i < NQ; ++i) {
-              float r;
-              if (in[i] && !lrn_fast_scale(bb[i], nbeta, r))
-                vv[i] = win[slot(j, LO)][i] / lrn_powf(bb[i], a.lrn_beta);
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-          if (i + 1 < NQ || static_cast<int>(threadIdx.x) + 256 * i < HpWp)
-            plane[j * HpWpE + wq[i]] = vv[i];
-        }
-      }
-    }
-    barrier_lds_only();  // planes written; unit b read by every wave
-    if (issued <= last_unit) dma(issued++);  // into unit b's slot
-    if (map && pk == 3)
-      pool_mapped<3, NM>(plane, ps, WpE, cbn * OHW, y + (n * a.C + c0) * OHW);
-    else if (map)
-      pool_mapped<2, NM>(plane, ps, WpE, cbn * OHW, y + (n * a.C + c0) * OHW);
-    else
-      pool_planes_step(plane, cbn, Hp, Wp, a, static_cast<int>(OH), static_cast<int>(OW),
-                       y + (n * a.C + c0) * OHW);
-    barrier_lds_only();  // planes free for the next block
-  }
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // no LDS-DMA outlives the workgroup
-}
-#endif  // FEDAGG_POOL_DMA
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -3621,20 +3373,7 @@ int fedagg_teacher_conv2d_f32(const float* x, int64_t x_kstride, const float* pa
         const int64_t tpx = (half ? 2 : 1) * kFlatThreads;
         const dim3 gflat(static_cast<unsigned>((nslots + tpx - 1) / tpx),
                          static_cast<unsigned>(oc_tiles), static_cast<unsigned>(kn));
-        const int64_t wp = s.OW + plan.ks - 1;
-        if (plan.ks == 5 && s.C == 3 && wp == 28 && plan.nrows == 20 && plan.xm == 16 &&
-            !half && ppad < 0) {
-          // SimpleCNN2's conv1 (3 x 24 x 24, 64 channels): compile-time geometry
-          hipLaunchKernelGGL((k_teacher_conv2d_flat<5, 3, 16, false, false, 28, 560>), gflat,
-                             dim3(kFlatThreads), plan.lds, st, xk, x_kstride, pk, params_kstride,
-                             w_off, b_off, s, plan.nslot, plan.nrows, yk, relu, ppad);
-        } else if (plan.ks == 5 && s.C == 1 && wp == 28 && plan.nrows == 56 && plan.xm == 8 &&
-                   half && ppad >= 0) {
-          // SimpleCNN's conv1 + pool (1 x 28 x 28, 32 channels)
-          hipLaunchKernelGGL((k_teacher_conv2d_flat<5, 1, 8, true, true, 28, 1568>), gflat,
-                             dim3(kFlatThreads), plan.lds, st, xk, x_kstride, pk, params_kstride,
-                             w_off, b_off, s, plan.nslot, plan.nrows, yk, relu, ppad);
-        } else if (plan.ks == 5) {
+        if (plan.ks == 5) {
           if (s.C == 3) {
             if (plan.xm == 8) FEDAGG_CONV_FLAT(5, 3, 8); else FEDAGG_CONV_FLAT(5, 3, 16);
           } else {
@@ -3750,38 +3489,6 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
     // planes with the pool padding as a border (k_pad_lrn_maxpool_slide)
     const size_t slds = static_cast<size_t>(cbs * (Hp + 2 * a.pool_ph) * (Wp + 2 * a.pool_pw)) *
                         sizeof(float);
-#ifdef FEDAGG_POOL_DMA
-    if ((a.H * a.W) % 4 == 0) {
-      for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {
-        const dim3 g(static_cast<unsigned>(G),
-                     static_cast<unsigned>(a.N - n0 < 65535 ? a.N - n0 : 65535));
-        const int64_t HWd = a.H * a.W;
-        const int64_t ple = (Hp + 2 * a.pool_ph) * (Wp + 2 * a.pool_pw);
-#define FEDAGG_POOL_D(SZ, Q, B, R)                                                          \
-  hipLaunchKernelGGL((k_pad_lrn_maxpool_dma<SZ, Q, B, R>), g, dim3(256),                    \
-                     static_cast<size_t>((R * B * HWd + B * ple) * 4), st, x, a, CG, OH, OW, \
-                     n0, y)
-#define FEDAGG_POOL_DQ(SZ)                                                     \
-  switch (nq) {                                                                \
-    case 1: FEDAGG_POOL_D(SZ, 1, FEDAGG_POOL_DMA_CB1, FEDAGG_POOL_DMA_RU); break; \
-    case 2: FEDAGG_POOL_D(SZ, 2, 8, FEDAGG_POOL_DMA_RU); break;                \
-    case 3: FEDAGG_POOL_D(SZ, 3, FEDAGG_POOL_DMA_CB3, FEDAGG_POOL_DMA_RU); break; \
-    default: FEDAGG_POOL_D(SZ, 4, 4, FEDAGG_POOL_DMA_RU);                      \
-  }
-        switch (a.lrn_size) {
-          case 0: FEDAGG_POOL_DQ(0); break;
-          case 3: FEDAGG_POOL_DQ(3); break;
-          case 4: FEDAGG_POOL_DQ(4); break;
-          default: FEDAGG_POOL_DQ(5);
-        }
-#undef FEDAGG_POOL_DQ
-#undef FEDAGG_POOL_D
-        const int rc = static_cast<int>(hipGetLastError());
-        if (rc) return rc;
-      }
-      return 0;
-    }
-#endif
     for (int64_t n0 = 0; n0 < a.N; n0 += 65535) {
       const dim3 g(static_cast<unsigned>(G),
                    static_cast<unsigned>(a.N - n0 < 65535 ? a.N - n0 : 65535));
