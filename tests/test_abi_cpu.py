@@ -322,3 +322,20 @@ def test_rejected_ab_flag_bits_are_gone():
     src = open(os.path.join(REPO, "fedsim_amd", "csrc", "fedagg_kernels.hip")).read()
     # no build-variant knob of a finished experiment is left in the kernels
     assert not re.search(r"^\s*#\s*if(n?def)?\b", src, re.M), "A/B build knobs in the kernels"
+
+
+def test_build_is_reproducible():
+    """The library is built with a fixed compilation-unit id, so identical
+    sources and flags give a byte-identical library (the md5 that keys
+    bench.py's PMC summary survives a rebuild).  tools/repro_build.py builds
+    twice from copies in different directories and records the md5s."""
+    import json
+
+    import __graft_entry__ as G
+
+    assert any(f.startswith("-cuid=") for f in G.HIP_FLAGS)
+    with open(os.path.join(REPO, "profiles", "r05_repro_build.json")) as f:
+        rec = json.load(f)
+    assert rec["identical"] and rec["builds"][0]["md5"] == rec["builds"][1]["md5"]
+    assert rec["builds"][0]["dir"] != rec["builds"][1]["dir"]
+    assert rec["flags"] == G.HIP_FLAGS
