@@ -25,11 +25,15 @@ LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
 # Must match include/fedagg.h
 ABI_VERSION = 4  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
 #                 3: the rejected flat-load / LDS-weight flag bits refused;
-#                 4: + fedagg_finalize_f64 (fp64 keys of the generic aggregator)
+#                 4: + fedagg_finalize_f64, fedagg_reduce_rows_ref (fp64 / bf16 /
+#                    fp16 keys of the generic aggregator)
 FEDAGG_INIT = 0x1
 FEDAGG_FINALIZE = 0x2
 FEDAGG_NT = 0x4
 FEDAGG_SCALAR = 0x8
+FEDAGG_DTYPE_BF16 = 1
+FEDAGG_DTYPE_F16 = 2
+FEDAGG_DTYPE_F64 = 3
 FEDAGG_UNROLL_SHIFT = 8
 FEDAGG_VPT_SHIFT = 12
 FEDAGG_BS_SHIFT = 14
@@ -167,6 +171,11 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p,
          ctypes.c_void_p],
+    ),
+    "fedagg_reduce_rows_ref": (
+        ctypes.c_int,
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
     ),
     "fedagg_finalize_f64": (
         ctypes.c_int,

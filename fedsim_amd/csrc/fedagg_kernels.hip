@@ -3070,6 +3070,124 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// The reference's arithmetic on bf16 / fp16 / fp64 client rows (the
+// dtype-generic SerialAggregator keys: aggregators.py:17-40 on such
+// tensors).  ATen computes ``value * weight`` and ``sum_v + new_v`` of
+// reduced-precision tensors in float (its opmath type) and rounds each result
+// to the tensor's dtype; fp64 rounds each in double.  Per column, in arrival
+// order:
+//   s_1     = rnd(rnd(x_0 * w_0) + 0)         (the reference's 0 + tensor)
+//   s_{k+1} = rnd(s_k + rnd(x_k * w_k))
+// with w_k = the Python weight in the opmath type (fl32 for bf16 / fp16).
+// No FMA (-ffp-contract=off): every product and sum rounds on its own.
+// ---------------------------------------------------------------------------
+struct RefBf16 {  // storage: the bf16 bits; opmath float
+  using T = uint16_t;
+  using OP = float;
+  static __device__ __forceinline__ float up(uint16_t u) {
+    return __builtin_bit_cast(float, static_cast<uint32_t>(u) << 16);
+  }
+  static __device__ __forceinline__ uint16_t down(float x) {  // c10::BFloat16's RNE
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    if (x != x) return 0x7FC0;
+    return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  }
+};
+struct RefF16 {  // storage: _Float16 (v_cvt_f16_f32: RNE); opmath float
+  using T = _Float16;
+  using OP = float;
+  static __device__ __forceinline__ float up(_Float16 h) { return static_cast<float>(h); }
+  static __device__ __forceinline__ _Float16 down(float x) { return static_cast<_Float16>(x); }
+};
+struct RefF64 {
+  using T = double;
+  using OP = double;
+  static __device__ __forceinline__ double up(double v) { return v; }
+  static __device__ __forceinline__ double down(double v) { return v; }
+};
+
+// One lane: VW consecutive columns [c, c + VW) of every row, U rows' loads in
+// flight; columns from c_lo.  Row pointers and weights are wave-uniform.
+template <class R, int VW, int U>
+__global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* const* __restrict__ rows,
+                                                         const typename R::OP* __restrict__ w,
+                                                         int64_t B, int64_t c_lo, int64_t P,
+                                                         const typename R::T* __restrict__ acc_in,
+                                                         typename R::T* __restrict__ out, int init) {
+  using T = typename R::T;
+  using OP = typename R::OP;
+  using V = T __attribute__((ext_vector_type(VW)));
+  const int64_t nvec = (P - c_lo) / VW;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
+       i += stride) {
+    const int64_t c = c_lo + i * VW;
+    OP s[VW];
+    int64_t k = 0;
+    if (init) {
+      const V x = *reinterpret_cast<const V*>(rows[0] + c);
+      const OP w0 = w[0];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const OP t = R::up(R::down(R::up(x[j]) * w0));
+        s[j] = R::up(R::down(t + OP(0)));
+      }
+      k = 1;
+    } else {
+      const V a = *reinterpret_cast<const V*>(acc_in + c);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) s[j] = R::up(a[j]);
+    }
+    for (; k + U <= B; k += U) {
+      V x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(rows[k + u] + c));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const OP wk = w[k + u];
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const OP t = R::up(R::down(R::up(x[u][j]) * wk));
+          s[j] = R::up(R::down(s[j] + t));
+        }
+      }
+    }
+    for (; k < B; ++k) {
+      const V x = __builtin_nontemporal_load(reinterpret_cast<const V*>(rows[k] + c));
+      const OP wk = w[k];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        const OP t = R::up(R::down(R::up(x[j]) * wk));
+        s[j] = R::up(R::down(s[j] + t));
+      }
+    }
+    V o;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) o[j] = R::down(s[j]);
+    *reinterpret_cast<V*>(out + c) = o;
+  }
+}
+
+template <class R, int VW>
+hipError_t launch_rows_ref(const void* const* rows, const void* w, int64_t B, int64_t P,
+                           const void* acc_in, void* out, bool init, bool vec, hipStream_t st) {
+  using T = typename R::T;
+  using OP = typename R::OP;
+  auto rt = reinterpret_cast<const T* const*>(rows);
+  auto wt = static_cast<const OP*>(w);
+  auto ai = static_cast<const T*>(acc_in);
+  auto ot = static_cast<T*>(out);
+  const int64_t body = vec ? P / VW * VW : 0;
+  if (body > 0)
+    hipLaunchKernelGGL((k_reduce_rows_ref<R, VW, 8>), dim3(elementwise_grid(body / VW)),
+                       dim3(kBlock), 0, st, rt, wt, B, int64_t(0), body, ai, ot, init ? 1 : 0);
+  if (body < P)  // columns past the last full vector (or every column: unaligned rows)
+    hipLaunchKernelGGL((k_reduce_rows_ref<R, 1, 8>), dim3(elementwise_grid(P - body)),
+                       dim3(kBlock), 0, st, rt, wt, B, body, P, ai, ot, init ? 1 : 0);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -3597,6 +3715,34 @@ int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out, void
   hipLaunchKernelGGL(k_finalize, dim3(elementwise_grid(P / 4 + 1)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), acc, W32, P, out);
   return static_cast<int>(hipGetLastError());
+}
+
+int fedagg_reduce_rows_ref(int dtype, const void* const* rows, const void* w, int64_t B,
+                           int64_t P, const void* acc_in, void* out, int flags, void* stream) {
+  const bool init = (flags & FEDAGG_INIT) != 0;
+  if (P < 0 || B < 0 || (init && B == 0)) return FEDAGG_EINVAL;
+  if (flags & ~(FEDAGG_INIT | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
+  if (P == 0) return 0;
+  if (!out || (!init && !acc_in) || (B > 0 && (!rows || !w))) return FEDAGG_EINVAL;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t es = dtype == FEDAGG_DTYPE_F64 ? 8 : 2;
+  if (B == 0) {  // nothing to add: the running sum as it is
+    if (out == acc_in) return 0;
+    return static_cast<int>(hipMemcpyAsync(out, acc_in, P * es, hipMemcpyDeviceToDevice, st));
+  }
+  // 16-B vectors where the caller vouches for the rows (no FEDAGG_SCALAR) and
+  // the accumulators are aligned too
+  const bool vec = !(flags & FEDAGG_SCALAR) && aligned16(out) && (init || aligned16(acc_in));
+  switch (dtype) {
+    case FEDAGG_DTYPE_BF16:
+      return static_cast<int>(launch_rows_ref<RefBf16, 8>(rows, w, B, P, acc_in, out, init, vec, st));
+    case FEDAGG_DTYPE_F16:
+      return static_cast<int>(launch_rows_ref<RefF16, 8>(rows, w, B, P, acc_in, out, init, vec, st));
+    case FEDAGG_DTYPE_F64:
+      return static_cast<int>(launch_rows_ref<RefF64, 2>(rows, w, B, P, acc_in, out, init, vec, st));
+    default:
+      return FEDAGG_EINVAL;
+  }
 }
 
 int fedagg_finalize_f64(const double* acc, double W, int64_t P, double* out, void* stream) {

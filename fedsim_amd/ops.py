@@ -29,6 +29,7 @@ __all__ = [
     "reduce_rows",
     "finalize",
     "finalize_f64",
+    "reduce_rows_ref",
     "fedavg_sgd",
     "adabest_sgd",
     "tuning_flags",
@@ -586,6 +587,50 @@ def finalize_f64(acc: torch.Tensor, W, out: Optional[torch.Tensor] = None) -> to
         acc.data_ptr(), float(W), acc.numel(), out.data_ptr(), _stream_ptr(acc.device)
     )
     check(rc, "fedagg_finalize_f64")
+    return out
+
+
+_REF_DTYPES = {torch.bfloat16: (_native.FEDAGG_DTYPE_BF16, torch.float32),
+               torch.float16: (_native.FEDAGG_DTYPE_F16, torch.float32),
+               torch.float64: (_native.FEDAGG_DTYPE_F64, torch.float64)}
+
+
+def reduce_rows_ref(rows: Sequence[torch.Tensor], weights: Sequence, out: torch.Tensor,
+                    acc_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The reference's ``add`` arithmetic over bf16 / fp16 / fp64 rows
+    (fedagg_reduce_rows_ref): ``out = acc_in + x_0 * w_0 + ...`` rounded per
+    product and per sum in the rows' dtype, in order; ``acc_in=None``: from
+    the reference's ``0 + first product``.  ``weights`` are the Python
+    weights (fl32 for bf16 / fp16, as ATen's opmath takes them)."""
+    if out.dtype not in _REF_DTYPES:
+        raise TypeError(f"reduce_rows_ref takes bf16 / fp16 / fp64 tensors, got {out.dtype}")
+    code, wdt = _REF_DTYPES[out.dtype]
+    dev = out.device
+    if dev.type != "cuda" or not out.is_contiguous():
+        raise ValueError("out must be a contiguous HIP tensor")
+    P, B = out.numel(), len(rows)
+    if len(weights) != B:
+        raise ValueError("one weight per row")
+    aligned = out.data_ptr() % 16 == 0
+    for i, r in enumerate(rows):
+        if r.dtype != out.dtype or r.device != dev or r.numel() != P or not r.is_contiguous():
+            raise ValueError(f"rows[{i}] must be a contiguous {out.dtype} tensor of {P} "
+                             f"elements on {dev}")
+        aligned = aligned and r.data_ptr() % 16 == 0
+    if acc_in is not None:
+        if acc_in.dtype != out.dtype or acc_in.device != dev or acc_in.numel() != P or \
+                not acc_in.is_contiguous():
+            raise ValueError("acc_in must match out")
+        aligned = aligned and acc_in.data_ptr() % 16 == 0
+    elif B == 0:
+        raise ValueError("no rows and no acc_in")
+    table = row_table_from_ptrs([r.data_ptr() for r in rows], dev) if B else None
+    wv = torch.tensor([fl32(w) if wdt == torch.float32 else float(w) for w in weights],
+                      dtype=wdt).pin_memory().to(dev, non_blocking=True) if B else None
+    flags = (FEDAGG_INIT if acc_in is None else 0) | (0 if aligned else FEDAGG_SCALAR)
+    rc = _native.load().fedagg_reduce_rows_ref(code, _ptr(table), _ptr(wv), B, P, _ptr(acc_in),
+                                               out.data_ptr(), flags, _stream_ptr(dev))
+    check(rc, "fedagg_reduce_rows_ref")
     return out
 
 

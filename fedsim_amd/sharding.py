@@ -443,6 +443,10 @@ class ShardedSerialAggregator(SerialAggregator):
         column slice of every vector, not whole rows)."""
         return None
 
+    def _new_ref_entry(self, value, weight):
+        """Non-fp32 keys stay replicated on the host path of every rank."""
+        return None
+
     @property
     def rank(self) -> int:
         return self._rank

@@ -312,6 +312,12 @@ class _TensorEntry(object):
 
     cur_w = 0
     dev = None
+    shape = ()
+
+    def takes(self, value, weight) -> bool:
+        """Whether this entry adds (value, weight) itself; otherwise the key
+        leaves it for the reference's arithmetic (SerialAggregator.add)."""
+        return _kernel_value(value, weight) and tuple(value.shape) == self.shape
 
 
 class _DeviceEntry(_TensorEntry):
@@ -747,6 +753,100 @@ def reference_quotient(v, w):
     return q.view(v.shape).to(out)
 
 
+def _ref_weight(weight) -> bool:
+    """A weight fedagg_reduce_rows_ref applies as ATen does: a real Python or
+    numpy number (converted to the opmath type)."""
+    return isinstance(weight, (int, float, np.integer, np.floating)) and not isinstance(
+        weight, complex)
+
+
+class _RefDeviceEntry(_TensorEntry):
+    """A HIP-resident key of bf16 / fp16 / fp64 tensors with real scalar
+    weights: the reference's arithmetic (aggregators.py:17-40, every product
+    and every sum rounded to the dtype, in arrival order) by
+    fedagg_reduce_rows_ref, in HBM, instead of two torch launches and three
+    passes per client.  ``add`` snapshots the value (the reference's clone,
+    training/utils.py:34) unless the aggregator borrows handed-over HBM
+    tensors; rows are reduced onto the running sum when ``max_rows`` or the
+    HBM budget are reached and at get / pop.  The sum and the quotient
+    (reference_quotient) are bitwise the reference's CPU tensors."""
+
+    DTYPES = (torch.bfloat16, torch.float16, torch.float64)
+
+    def __init__(self, value: torch.Tensor, opts: _Options):
+        self.shape = tuple(value.shape)
+        self.dtype = value.dtype
+        self.dev = value.device
+        self.out_device = value.device
+        self.P = value.numel()
+        self.borrow = opts.borrow
+        budget = _slab_budget(self.dev, opts.slab_bytes)
+        self.Bmax = max(1, min(opts.max_rows, budget // max(1, self.P * value.element_size())))
+        self.rows: List = []  # (tensor, version or None)
+        self.ws: List = []
+        self.acc: Optional[torch.Tensor] = None
+        self.cur_w = 0
+
+    def takes(self, value, weight) -> bool:
+        return (isinstance(value, torch.Tensor) and value.dtype == self.dtype
+                and value.device == self.dev and tuple(value.shape) == self.shape
+                and _ref_weight(weight))
+
+    def add(self, value: torch.Tensor, weight) -> None:
+        new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
+        src = value.detach() if value.requires_grad else value
+        src = src.reshape(-1)
+        if self.borrow and src.is_contiguous():
+            row = (src, src._version)  # handed over: read at the reduction
+        else:
+            row = (src.clone(memory_format=torch.contiguous_format), None)
+        self.rows.append(row)
+        self.ws.append(weight)
+        self.cur_w = new_w
+        if len(self.rows) >= self.Bmax:
+            self._drain()
+
+    def _drain(self) -> None:
+        if not self.rows:
+            return
+        rows = []
+        for t, version in self.rows:
+            if version is not None and t._version != version:
+                raise RuntimeError(
+                    "a client tensor was modified in place after SerialAggregator.add(); "
+                    "an aggregator created with borrow=True reads it when the round is "
+                    "reduced (use borrow=False to snapshot it at add time)")
+            rows.append(t)
+        out = self.acc if self.acc is not None else torch.empty(self.P, dtype=self.dtype,
+                                                                device=self.dev)
+        ops.reduce_rows_ref(rows, self.ws, out, acc_in=self.acc)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        _keep_until(ev, rows)  # the rows stay alive until the reduction ran
+        self.acc = out
+        self.rows, self.ws = [], []
+
+    def _weighted(self) -> bool:
+        return not (self.cur_w is None or self.cur_w == 0)
+
+    def get_sum(self) -> torch.Tensor:
+        self._drain()
+        return self.acc.view(self.shape).clone()
+
+    def get(self) -> torch.Tensor:
+        s = self.get_sum()
+        return reference_quotient(s, self.cur_w) if self._weighted() else s
+
+    def pop(self, on_device: bool = False) -> torch.Tensor:
+        self._drain()
+        s = self.acc.view(self.shape)
+        self.acc = None
+        return reference_quotient(s, self.cur_w) if self._weighted() else s
+
+    def pop_step(self, step: ops.ServerStep) -> None:
+        step.apply(self.pop().reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+
+
 def _drop_entry(entry) -> None:
     release = getattr(entry, "release", None)
     if release is not None:
@@ -804,6 +904,16 @@ class SerialAggregator(object):
         """State of a new tensor-valued key (sharded aggregators override)."""
         return _DeviceEntry(value, _hip_device(value, self._opts.device), self._opts, self)
 
+    def _new_ref_entry(self, value, weight) -> Optional[_TensorEntry]:
+        """A HIP bf16 / fp16 / fp64 key with a real scalar weight: the
+        reference's arithmetic in HBM (_RefDeviceEntry); None otherwise (the
+        sharded aggregators keep such keys on the host path)."""
+        if (isinstance(value, torch.Tensor) and value.dim() > 0 and value.device.type == "cuda"
+                and value.dtype in _RefDeviceEntry.DTYPES and _ref_weight(weight)
+                and type(value) is torch.Tensor):
+            return _RefDeviceEntry(value, self._opts)
+        return None
+
     @staticmethod
     def _is_device_value(value, weight=1) -> bool:
         """Whether an add of (value, weight) to a new key starts a kernel
@@ -850,7 +960,7 @@ class SerialAggregator(object):
             else:
                 res.release()  # a reserved row still alive keeps a copy
         if isinstance(entry, _TensorEntry):
-            if self._is_device_value(value, weight) and tuple(value.shape) == entry.shape:
+            if entry.takes(value, weight):
                 entry.add(value, weight)
                 return
             # the key leaves the kernel path (a value of another dtype or
@@ -866,8 +976,14 @@ class SerialAggregator(object):
             entry.add(value, weight)
             self._members[key] = entry
             return
+        if entry is None:
+            entry = self._new_ref_entry(value, weight)
+            if entry is not None:
+                entry.add(value, weight)  # may raise (weight None): the key is not created
+                self._members[key] = entry
+                return
         # the reference's own arithmetic (aggregators.py:17-40) on the
-        # value's device: scalars, 0-dim and non-fp32 tensors
+        # value's device: scalars, 0-dim tensors, host tensors of other dtypes
         self._members[key] = reference_add(self._members.get(key, (0, 0)), value, weight)
 
     def _entry(self, key):

@@ -16,6 +16,9 @@
  *       same, over a column-blocked HBM slab layout
  *   fedagg_finalize_f32 / fedagg_finalize_f64
  *       replaces SerialAggregator.get/pop's v / w  fedsim/utils/aggregators.py:56-60,118-122
+ *   fedagg_reduce_rows_ref
+ *       SerialAggregator.add on bf16 / fp16 / fp64 tensor keys, the reference's
+ *       rounding per product and per add                  aggregators.py:17-40
  *   fedagg_fedavg_sgd_f32
  *       replaces FedAvg.optimize's pseudo-grad + torch.optim.SGD.step
  *                                                  fedsim/distributed/centralized/training/fedavg.py:199-203
@@ -60,8 +63,9 @@ extern "C" {
    (linear, conv2d, pad-LRN-maxpool) and slab-row (pack_segments, unpack_row)
    entry points and their structs; 3: flag bits 0x10000 / 0x20000 (the
    flat-load and LDS-weight A/B switches, measured and rejected) are no
-   longer accepted (FEDAGG_EINVAL); 4: + fedagg_finalize_f64 (the reference's
-   v / w for fp64 keys of the dtype-generic SerialAggregator) */
+   longer accepted (FEDAGG_EINVAL); 4: + fedagg_finalize_f64 and
+   fedagg_reduce_rows_ref (the dtype-generic SerialAggregator's fp64 / bf16 /
+   fp16 keys) */
 #define FEDAGG_ABI_VERSION 4
 
 /* flags for the reduce entry points */
@@ -334,6 +338,26 @@ int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out,
  */
 int fedagg_finalize_f64(const double* acc, double W, int64_t P, double* out,
                         void* stream);
+
+/*
+ * The reference's SerialAggregator arithmetic on bf16 / fp16 / fp64 rows
+ * (aggregators.py:17-40 for a key whose values are such tensors: an fp64 or
+ * bf16 model).  ATen rounds every ``value * weight`` and every ``sum + new``
+ * to the dtype (computing in float, its opmath type, for bf16 / fp16; in
+ * double for fp64), so per column, in arrival order:
+ *     s_1 = rnd(rnd(x_0 * w_0) + 0),   s_{k+1} = rnd(s_k + rnd(x_k * w_k))
+ * rows: DEVICE table of B pointers to P elements of the dtype; w: B DEVICE
+ * weights, float (fl32 of the Python weight) for BF16 / F16, double for F64;
+ * acc_in: the running sum s_k (ignored with FEDAGG_INIT, which starts the
+ * chain with the first row); out may alias acc_in.  flags: FEDAGG_INIT,
+ * FEDAGG_SCALAR (some row not 16-B aligned: element loads only).  Bitwise
+ * equal to the reference's CPU tensors.
+ */
+#define FEDAGG_DTYPE_BF16 1
+#define FEDAGG_DTYPE_F16  2
+#define FEDAGG_DTYPE_F64  3
+int fedagg_reduce_rows_ref(int dtype, const void* const* rows, const void* w, int64_t B,
+                           int64_t P, const void* acc_in, void* out, int flags, void* stream);
 
 /*
  * FedAvg server step with plain SGD (no momentum / weight decay / nesterov):

@@ -46,7 +46,7 @@ def test_header_declares_the_abi():
         "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_teacher_conv2d_f32",
         "fedagg_conv_stage", "fedagg_conv_order", "fedagg_conv_pool_fusable", "fedagg_pool_output",
         "fedagg_pad_lrn_maxpool_f32",
-        "fedagg_finalize_f32", "fedagg_finalize_f64",
+        "fedagg_finalize_f32", "fedagg_finalize_f64", "fedagg_reduce_rows_ref",
         "fedagg_fedavg_sgd_f32",
         "fedagg_adabest_sgd_f32", "fedagg_feddyn_sgd_f32", "fedagg_server_step_f32",
         "fedagg_reduce_step_blocked_f32", "fedagg_reduce_step_rows_f32",

@@ -148,3 +148,43 @@ def test_dtype_round_loop_gpu(run, device):
         assert t.device.type == device
         assert G.encode(t) == run["outputs"][k], k
     assert {k: G.encode(v) for k, v in scores.items()} == run["scores"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float64"])
+@pytest.mark.parametrize("borrow,max_rows", [(False, 4096), (False, 5), (True, 4096), (True, 3)])
+def test_hbm_reference_arithmetic_kernel(dtype, borrow, max_rows):
+    """bf16 / fp16 / fp64 keys in HBM run fedagg_reduce_rows_ref (the
+    reference's rounding per product and per add, arrival order), drained in
+    pieces onto the running sum when max_rows is reached: bitwise the
+    reference's CPU aggregation of the same values, including an odd P (the
+    scalar tail), a 4-byte-offset row (element loads) and get() mid-stream."""
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _RefDeviceEntry
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    K, P = 23, 100_003
+    g = torch.Generator().manual_seed(3)
+    X = [(torch.randn(P, generator=g, dtype=torch.float64) * 0.5).to(dt) for _ in range(K)]
+    w = [int(v) for v in torch.randint(1, 600, (K,), generator=g)]
+    w[3] = 2.75  # a float weight
+    ref = ReferenceSerialAggregator()
+    agg = SerialAggregator(borrow=borrow, max_rows=max_rows)
+    big = torch.empty(P + 2, dtype=dt, device=dev)
+    for k in range(K):
+        if k == 7:  # a row at an offset of one element: not 16-B aligned
+            big[1:P + 1].copy_(X[k])
+            v = big[1:P + 1]
+        else:
+            v = X[k].to(dev)
+        agg.add("p", v, w[k])
+        ref.add("p", X[k], w[k])
+        if k == 11:
+            assert G.encode(agg.get("p")) == G.encode(ref.get("p"))
+    assert isinstance(agg._members["p"], _RefDeviceEntry)
+    assert G.encode(agg.get_sum("p")) == G.encode(ref.get_sum("p"))
+    assert agg.get_weight("p") == ref.get_weight("p")
+    got = agg.pop("p")
+    assert got.device == dev and got.dtype == dt
+    assert G.encode(got) == G.encode(ref.pop("p"))
