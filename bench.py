@@ -527,6 +527,9 @@ def multi_gpu_selftest(rk, fault_rank=None):
                           running sum passed rank to rank + broadcast  bitwise
       client_allreduce    mode="allreduce": partial sums + RCCL all-reduce
                           (reordered)                        normwise <= 1e-6
+      client_bf16_key     a bf16 key in a client-sharded round: the
+                          reference's arithmetic, chained as raw bytes
+                          (vs oracle/reference_loop)                 bitwise
       param_sharded_step  sharding.param_sharded_step on this rank's column
                           shard (blocked slab, fused step)           bitwise
 
@@ -588,6 +591,23 @@ def multi_gpu_selftest(rk, fault_rank=None):
                 (P,), torch.float32, "cpu" if rk.rehearsal else "cuda", owner[k])
             agg.add("p", v, w[k])
         record("client_" + mode, agg.pop("p").cpu().numpy(), avg_ref, bitwise=mode == "chain")
+    # a bf16 key (a bf16 model's vectors) in the same client-sharded round:
+    # the reference's arithmetic, its running sum chained rank to rank as raw
+    # bytes (sharding._ClientShardRef), against the reference restatement
+    from oracle.reference_loop import ReferenceSerialAggregator
+
+    Xh = torch.from_numpy(X).to(torch.bfloat16)
+    refagg = ReferenceSerialAggregator()
+    agg = ClientShardedSerialAggregator(mode="allreduce", **kw,
+                                        **(dict(step_impl=_oracle_step) if entry else {}))
+    for k in range(K):
+        refagg.add("h", Xh[k], w[k])
+        v = Xh[k].to(dev) if owner[k] == me else RemoteRow(
+            (P,), torch.bfloat16, "cpu" if rk.rehearsal else "cuda", owner[k])
+        agg.add("h", v, w[k])
+    got, want = agg.pop("h").cpu(), refagg.pop("h")
+    bad = int((got.view(torch.int16) != want.view(torch.int16)).sum())
+    checks["client_bf16_key"] = dict(bitwise=True, columns=P, mismatched=bad, ok=bad == 0)
     # (3) the parameter-sharded round step of bench's own headline mode
     lo, hi = sharding.shard_range(P, me, world, sharding.ALIGN)
     w32 = torch.tensor([ops.fl32(v) for v in w], dtype=torch.float32, device=dev)

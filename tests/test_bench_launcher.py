@@ -44,7 +44,7 @@ def test_launcher_one_line(mode, gpus):
 
 
 SELFTEST_CHECKS = {"sharded_pop_step", "sharded_pop_step_grad", "client_chain",
-                   "client_allreduce", "param_sharded_step"}
+                   "client_allreduce", "client_bf16_key", "param_sharded_step"}
 
 
 def _selftest_ok(d, world):
