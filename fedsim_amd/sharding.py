@@ -164,8 +164,8 @@ def weights_fp32(weights: Sequence, device) -> torch.Tensor:
 # plugin surface: a parameter-sharded SerialAggregator
 # ---------------------------------------------------------------------------
 from .utils.aggregators import (  # noqa: E402
-    SerialAggregator, _DeviceEntry, _hip_device, _kernel_value, _TensorEntry, reference_add,
-    reference_quotient)
+    SerialAggregator, _DeviceEntry, _hip_device, _kernel_value, _ref_weight, _RefDeviceEntry,
+    _TensorEntry, reference_add, reference_quotient)
 
 
 def _group_rank_world(group):
@@ -182,17 +182,27 @@ class _ShardEntry(_TensorEntry):
     own device); results are assembled with one all-gather of the equal-width
     shards."""
 
-    def __init__(self, agg: "ShardedSerialAggregator", value: torch.Tensor):
+    def __init__(self, agg: "ShardedSerialAggregator", value: torch.Tensor, ref: bool = False):
         self.agg = agg
         self.shape = tuple(value.shape)
         self.P = value.numel()
+        self.dtype = value.dtype if ref else torch.float32
+        self.ref = ref  # a bf16 / fp16 / fp64 key: _RefDeviceEntry on the slice
         self.out_device = value.device
         self.lo, self.hi = shard_span(self.P, agg._rank, agg._world)
         self.S = shard_width(self.P, agg._world)
         self.cur_w = 0
-        self.inner = agg._shard_entry(value.reshape(-1)[self.lo:self.hi]) \
-            if self.hi > self.lo else None
+        part = value.reshape(-1)[self.lo:self.hi]
+        self.inner = None if self.hi <= self.lo else (
+            _RefDeviceEntry(part, agg._opts) if ref else agg._shard_entry(part))
         self.dev = self.inner.dev if self.inner is not None else agg._device_for(value)
+
+    def takes(self, value, weight) -> bool:
+        if not self.ref:
+            return super().takes(value, weight)
+        return (isinstance(value, torch.Tensor) and value.dtype == self.dtype
+                and value.device == self.out_device and tuple(value.shape) == self.shape
+                and _ref_weight(weight))
 
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
@@ -224,7 +234,7 @@ class _ShardEntry(_TensorEntry):
         return full
 
     def _assemble(self, part: Optional[torch.Tensor]) -> torch.Tensor:
-        full = torch.empty(self.P, dtype=torch.float32, device=self.dev)
+        full = torch.empty(self.P, dtype=self.dtype, device=self.dev)
         self._gather_into(full, part)
         return full
 
@@ -444,7 +454,16 @@ class ShardedSerialAggregator(SerialAggregator):
         return None
 
     def _new_ref_entry(self, value, weight):
-        """Non-fp32 keys stay replicated on the host path of every rank."""
+        """A HIP bf16 / fp16 / fp64 key with a real scalar weight: each rank
+        reduces its column slice with the reference's arithmetic
+        (_RefDeviceEntry), assembled like the fp32 keys.  Single-process
+        shards keep such keys on the host path."""
+        if self._devices is not None or self._entry_factory is not None:
+            return None
+        if (isinstance(value, torch.Tensor) and value.dim() > 0 and value.device.type == "cuda"
+                and value.dtype in _RefDeviceEntry.DTYPES and _ref_weight(weight)
+                and type(value) is torch.Tensor):
+            return _ShardEntry(self, value, ref=True)
         return None
 
     @property

@@ -551,3 +551,114 @@ def test_chained_entry_grows_without_draining(where):
     got = e.partial(torch.from_numpy(acc0.copy()).to(dev), W=sum(w))
     want = ref.reduce(X, w, acc_in=acc0.copy(), W=sum(w))
     np.testing.assert_array_equal(bits(got.cpu().numpy()), bits(want))
+
+
+def _dtype_runs():
+    import json
+
+    from conftest import GOLDEN_DIR
+
+    with open(os.path.join(GOLDEN_DIR, "generic_keys.json")) as f:
+        return json.load(f)["dtype_runs"]
+
+
+def _dtype_round(run, factory):
+    import random
+    from functools import partial
+
+    from fedsim_amd.distributed.centralized import training
+    from oracle import generic_cases as G
+    from oracle import synthetic_fl as S
+
+    cls = S.make_algorithm(getattr(training, run["algorithm"]))
+    random.seed(S.RANDOM_SEED)
+    torch.manual_seed(S.TORCH_SEED)
+    alg = cls(data_manager=S.FakeDataManager(), metric_logger=None, num_clients=S.NUM_CLIENTS,
+              sample_scheme="uniform", sample_rate=S.SAMPLE_RATE,
+              model_def=S.MODELS[run["model"]], epochs=1, criterion_def="CrossEntropyScore",
+              optimizer_def=partial(torch.optim.SGD, **run["opt_kwargs"]), device="cuda",
+              aggregator_factory=factory, **run["alg_kwargs"])
+    scores = alg.train(rounds=S.ROUNDS)
+    st = alg.get_server_storage()
+    cloud = st.read("cloud_params")
+    got = dict(cloud=G.encode(cloud.detach()))
+    if run["algorithm"] == "AdaBest":
+        got["avg_params"] = G.encode(st.read("avg_params"))
+    buf = st.read("optimizer").state[cloud].get("momentum_buffer")
+    if buf is not None:
+        got["momentum_buffer"] = G.encode(buf)
+    return got, {k: G.encode(v) for k, v in scores.items()}
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float64"])
+def test_sharded_generic_key_one_rank(dtype, pg):
+    """A bf16 / fp16 / fp64 key under the parameter-sharded aggregator (one
+    RCCL rank): the slice reduced with the reference's arithmetic in HBM
+    (_RefDeviceEntry), assembled by the all-gather; then an fp32 value makes
+    the key leave it (collective get_sum, torch's promotion) -- bitwise the
+    reference's CPU aggregation throughout."""
+    from fedsim_amd.sharding import ShardedSerialAggregator, _ShardEntry
+    from oracle.generic_cases import encode
+    from oracle.reference_loop import ReferenceSerialAggregator
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    K, P = 13, 70_001
+    g = torch.Generator().manual_seed(9)
+    X = [(torch.randn(P, generator=g, dtype=torch.float64) * 0.3).to(dt) for _ in range(K)]
+    w = [int(v) for v in torch.randint(1, 300, (K,), generator=g)]
+    agg, ref = ShardedSerialAggregator(borrow=True, max_rows=4), ReferenceSerialAggregator()
+    for k in range(K):
+        agg.add("p", X[k].to(dev), w[k])
+        ref.add("p", X[k], w[k])
+    e = agg._members["p"]
+    assert isinstance(e, _ShardEntry) and e.ref
+    assert encode(agg.get_sum("p")) == encode(ref.get_sum("p"))
+    assert encode(agg.get("p")) == encode(ref.get("p"))
+    f32 = torch.randn(P, generator=g)
+    agg.add("p", f32.to(dev), 3)  # leaves the kernel: promotion as the reference
+    ref.add("p", f32, 3)
+    assert encode(agg.pop("p")) == encode(ref.pop("p"))
+
+
+def _gloo_dtype_worker(rank, world, port, outdir):
+    import json
+    from functools import partial
+
+    import torch.distributed as dist
+
+    from fedsim_amd.sharding import ShardedSerialAggregator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        for run in _dtype_runs():
+            got, scores = _dtype_round(run, partial(ShardedSerialAggregator, borrow=True))
+            out[run["id"]] = dict(outputs=got, scores=scores)
+        with open(os.path.join(outdir, f"dtype_rank{rank}.json"), "w") as f:
+            json.dump(out, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_dtype_rounds_two_ranks_on_one_gpu():
+    """fp64 / bf16 models through the parameter-sharded round driver, two
+    gloo ranks sharing the GPU: each rank reduces half of every fp64 / bf16
+    client vector in HBM with the reference's arithmetic; after 5 rounds
+    both hold the reference's server state bit for bit."""
+    import json
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_gloo_dtype_worker, args=(2, _port(), d), nprocs=2, join=True,
+                           start_method="spawn")
+        for r in range(2):
+            with open(os.path.join(d, f"dtype_rank{r}.json")) as f:
+                got = json.load(f)
+            for run in _dtype_runs():
+                assert got[run["id"]]["outputs"] == run["outputs"], (run["id"], r)
+                assert got[run["id"]]["scores"] == run["scores"], (run["id"], r)
