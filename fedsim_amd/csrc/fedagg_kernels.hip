@@ -3082,29 +3082,44 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 // with w_k = the Python weight in the opmath type (fl32 for bf16 / fp16).
 // No FMA (-ffp-contract=off): every product and sum rounds on its own.
 // ---------------------------------------------------------------------------
+// up: a stored element in the opmath type; rnd: an opmath value rounded to
+// the dtype, kept in the opmath type; store: the dtype's bits of an already
+// rounded value, a NaN as ATen's conversion writes it.  A NaN anywhere in a
+// column's chain stays NaN to the end, so the hardware conversions (RNE,
+// denormals kept) round every step and only the stored NaN is canonicalised.
 struct RefBf16 {  // storage: the bf16 bits; opmath float
   using T = uint16_t;
   using OP = float;
   static __device__ __forceinline__ float up(uint16_t u) {
     return __builtin_bit_cast(float, static_cast<uint32_t>(u) << 16);
   }
-  static __device__ __forceinline__ uint16_t down(float x) {  // c10::BFloat16's RNE
-    const uint32_t u = __builtin_bit_cast(uint32_t, x);
-    if (x != x) return 0x7FC0;
-    return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  static __device__ __forceinline__ float rnd(float x) {  // v_cvt_pk_bf16_f32
+    return up(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)));
+  }
+  static __device__ __forceinline__ uint16_t store(float x) {  // c10::BFloat16: NaN -> 0x7FC0
+    return x != x ? uint16_t(0x7FC0) : __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));
   }
 };
-struct RefF16 {  // storage: _Float16 (v_cvt_f16_f32: RNE); opmath float
-  using T = _Float16;
+struct RefF16 {  // storage: the fp16 bits; opmath float
+  using T = uint16_t;
   using OP = float;
-  static __device__ __forceinline__ float up(_Float16 h) { return static_cast<float>(h); }
-  static __device__ __forceinline__ _Float16 down(float x) { return static_cast<_Float16>(x); }
+  static __device__ __forceinline__ float up(uint16_t u) {
+    return static_cast<float>(__builtin_bit_cast(_Float16, u));
+  }
+  static __device__ __forceinline__ float rnd(float x) {  // v_cvt_f16_f32
+    return static_cast<float>(static_cast<_Float16>(x));
+  }
+  static __device__ __forceinline__ uint16_t store(float x) {  // c10::Half: NaN -> sign | 0x7E00
+    if (x != x) return static_cast<uint16_t>((__builtin_bit_cast(uint32_t, x) >> 16) & 0x8000u) | 0x7E00u;
+    return __builtin_bit_cast(uint16_t, static_cast<_Float16>(x));
+  }
 };
 struct RefF64 {
   using T = double;
   using OP = double;
   static __device__ __forceinline__ double up(double v) { return v; }
-  static __device__ __forceinline__ double down(double v) { return v; }
+  static __device__ __forceinline__ double rnd(double v) { return v; }
+  static __device__ __forceinline__ double store(double v) { return v; }
 };
 
 // One lane: VW consecutive columns [c, c + VW) of every row, U rows' loads in
@@ -3118,6 +3133,7 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
   using T = typename R::T;
   using OP = typename R::OP;
   using V = T __attribute__((ext_vector_type(VW)));
+  using GV = const __attribute__((address_space(1))) V;  // global loads, not flat
   const int64_t nvec = (P - c_lo) / VW;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
@@ -3126,12 +3142,12 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
     OP s[VW];
     int64_t k = 0;
     if (init) {
-      const V x = *reinterpret_cast<const V*>(rows[0] + c);
+      const V x = *(GV*)(rows[0] + c);
       const OP w0 = w[0];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
-        const OP t = R::up(R::down(R::up(x[j]) * w0));
-        s[j] = R::up(R::down(t + OP(0)));
+        const OP t = R::rnd(R::up(x[j]) * w0);
+        s[j] = R::rnd(t + OP(0));
       }
       k = 1;
     } else {
@@ -3142,29 +3158,29 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
     for (; k + U <= B; k += U) {
       V x[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(rows[k + u] + c));
+      for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load((GV*)(rows[k + u] + c));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const OP wk = w[k + u];
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
-          const OP t = R::up(R::down(R::up(x[u][j]) * wk));
-          s[j] = R::up(R::down(s[j] + t));
+          const OP t = R::rnd(R::up(x[u][j]) * wk);
+          s[j] = R::rnd(s[j] + t);
         }
       }
     }
     for (; k < B; ++k) {
-      const V x = __builtin_nontemporal_load(reinterpret_cast<const V*>(rows[k] + c));
+      const V x = __builtin_nontemporal_load((GV*)(rows[k] + c));
       const OP wk = w[k];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
-        const OP t = R::up(R::down(R::up(x[j]) * wk));
-        s[j] = R::up(R::down(s[j] + t));
+        const OP t = R::rnd(R::up(x[j]) * wk);
+        s[j] = R::rnd(s[j] + t);
       }
     }
     V o;
 #pragma unroll
-    for (int j = 0; j < VW; ++j) o[j] = R::down(s[j]);
+    for (int j = 0; j < VW; ++j) o[j] = R::store(s[j]);
     *reinterpret_cast<V*>(out + c) = o;
   }
 }
