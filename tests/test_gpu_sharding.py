@@ -662,3 +662,19 @@ def test_sharded_dtype_rounds_two_ranks_on_one_gpu():
             for run in _dtype_runs():
                 assert got[run["id"]]["outputs"] == run["outputs"], (run["id"], r)
                 assert got[run["id"]]["scores"] == run["scores"], (run["id"], r)
+
+
+def test_client_storage_tensor_arrives_as_a_leaf():
+    """A client-storage tensor another rank wrote (host copy, requires_grad)
+    is moved to this rank's GPU as a LEAF that requires grad, as the
+    reference's own storage would hold it (an optimizer accepts it and its
+    .grad fills in)."""
+    from fedsim_amd.distributed.centralized.centralized_fl_algorithm import _from_host
+
+    host = torch.arange(4.0).requires_grad_(True)
+    t = _from_host(("__fedsim_tensor__", host, "cuda", True), torch.device("cuda:0"))
+    assert t.device.type == "cuda" and t.is_leaf and t.requires_grad
+    opt = torch.optim.SGD([t], lr=0.5)
+    (t * t).sum().backward()
+    opt.step()
+    assert torch.equal(t.detach().cpu(), torch.arange(4.0) - 0.5 * 2 * torch.arange(4.0))
