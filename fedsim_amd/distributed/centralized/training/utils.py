@@ -39,6 +39,7 @@ from ....local import local_inference
 from ....utils import initialize_module, vectorize_module
 from ....utils.aggregators import SerialAggregator as _DeviceSerialAggregator
 from ....utils.handover import take_token, unaliased
+from ....utils.slab_rows import SlabRow
 
 
 def serial_aggregation(
@@ -108,6 +109,12 @@ def _handed_over(t: torch.Tensor) -> bool:
     secondary guard, the message holding the only reference to ``t``
     (calibrated reference count, _owned_refs) and no alias.  Called with
     serial_aggregation's ``params`` local, as _owned_refs measures."""
+    if isinstance(t, SlabRow) and t.in_slab and not t._committed:
+        # a row the client reserved in the round's slab (reserve_round_row):
+        # handed over by that protocol -- it is the aggregator's own memory,
+        # and torch ops on the SlabRow afterwards act on a private copy
+        take_token(t)
+        return True
     token = take_token(t)
     if token is not None:
         return token and unaliased(t)

@@ -54,6 +54,8 @@ def vectorize_module(module: Module, clone=True, detach=True, out=None) -> Tenso
 
         if not isinstance(out, SlabRow) or not out.in_slab:
             raise TypeError("out must be a reserved SlabRow still in its slab")
+        if out._committed:  # its contents are the aggregator's now
+            raise ValueError("out was already added to the aggregator; reserve a new row")
         params = [p.detach() for p in module.parameters()]
         P = sum(p.numel() for p in params)
         if P != out.shape[0]:

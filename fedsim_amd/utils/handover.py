@@ -19,8 +19,12 @@ as handed over only if
   base it is a view of: ``_base`` / the storage's use count);
 * no earlier vector of the round was handed over from the same storage.
 
-Anything else -- a vector without a token (a user client that did not
-declare it), a changed one, an aliased one -- gets the reference's clone.
+A row the client reserved in the round's slab (``reserve_round_row`` +
+``vectorize_module(out=row)``) is handed over by that protocol: it is the
+aggregator's memory, a committed row cannot be written again, and torch ops
+on the SlabRow act on a private copy.  Anything else -- a vector without a
+token (a user client that did not declare it), a changed one, an aliased one
+-- gets the reference's clone.
 A producer that calls ``hand_over`` and still changes the very tensor in
 place before the round is reduced breaks its declaration: the version
 counter makes that reduction raise instead of reading changed data.

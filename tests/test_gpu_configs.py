@@ -279,7 +279,7 @@ def _gpu_slab_client(record, cols, slab_row=True):
     the aggregator borrows in place).  Records (vector[cols], weight)."""
     from torch.nn.utils import parameters_to_vector, vector_to_parameters
 
-    from fedsim_amd.utils import vectorize_module
+    from fedsim_amd.utils import hand_over, vectorize_module
     from fedsim_amd.utils.slab_rows import reserve_round_row
 
     def send_to_server(id, rounds, storage, datasets, train_split_name, scores, epochs,
@@ -296,7 +296,10 @@ def _gpu_slab_client(record, cols, slab_row=True):
             assert row is not None and row.in_slab
         n = len(datasets[train_split_name])
         record.append((local[cols], n))
-        return dict(local_params=vectorize_module(model, out=row), num_steps=max(1, n // 32),
+        # a fresh vector the client keeps nowhere: declared handed over, so
+        # the round driver's aggregator reads it where it lies (borrowed)
+        return dict(local_params=hand_over(vectorize_module(model, out=row)),
+                    num_steps=max(1, n // 32),
                     diverged=False, num_samples={train_split_name: n},
                     metrics={train_split_name: {"loss": 1.0 + 0.001 * id}})
 

@@ -287,3 +287,21 @@ def test_slab_rows_carry_special_values_bitwise():
     nan = np.isnan(exp)
     assert nan.any() and np.array_equal(np.isnan(out), nan)  # NaN payloads may differ
     np.testing.assert_array_equal(bits(out[~nan]), bits(exp[~nan]))
+
+
+def test_committed_row_cannot_be_written_again():
+    """A reserved row is handed over by the reservation protocol: once added
+    it belongs to the aggregator -- packing into it again raises, and torch
+    ops on the SlabRow act on a private copy (the slab keeps the sum's bits)."""
+    from fedsim_amd.utils import vectorize_module
+
+    torch.manual_seed(3)
+    m = torch.nn.Linear(40, 7).to(DEV)
+    v = torch.nn.utils.parameters_to_vector(m.parameters()).detach().clone()
+    agg = _agg(expected_rows=2)
+    row = vectorize_module(m, out=agg.reserve("p", v.numel(), DEV))
+    agg.add("p", row, 2)
+    with pytest.raises(ValueError, match="already added"):
+        vectorize_module(m, out=row)
+    row.mul_(0)  # acts on the row's own copy, not on the slab
+    assert torch.equal(agg.pop("p"), (0 + v * 2) / 2)
