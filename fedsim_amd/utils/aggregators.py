@@ -362,6 +362,7 @@ class _DeviceEntry(_TensorEntry):
         self.rows = RowRefs()        # SlabRows handed out by reserve()
         self.copy_event = None       # last host DMA into the slab (copy stream)
         self.staging: List[Future] = []  # ingest-worker puts not yet checked
+        self.failed: Optional[BaseException] = None  # a failed put: the ring is incomplete
         self.last_flush_event = None  # last reduction reading the slab (compute stream)
         self.wait_before_copy = None
 
@@ -372,13 +373,16 @@ class _DeviceEntry(_TensorEntry):
         put is checked, not only the last: the first failure (a tensor
         modified in place, an allocation or HIP error) is raised here, so a
         row that was never written cannot reach a reduction."""
+        if self.failed is not None:  # a row was never written: every later use refuses
+            raise self.failed
         if self.staging:
             futs, self.staging = self.staging, []
             _wait_futures(futs)
             for f in futs:
                 if f.exception() is not None:
                     self.copy_event = None
-                    raise f.exception()
+                    self.failed = f.exception()
+                    raise self.failed
         if isinstance(self.copy_event, Future):
             self.copy_event = self.copy_event.result()
 

@@ -551,7 +551,9 @@ def test_earlier_handed_over_row_failure_is_not_lost(dev, pinned):
     a.mul_(3)
     gate.set()
     with pytest.raises(RuntimeError, match="modified in place"):
-        agg.pop("p")
+        agg.get("p")
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.pop("p")  # still refused: the ring lacks that row
     # the next round's aggregator is unaffected
     agg = SerialAggregator(borrow=True, borrow_host=True)
     agg.add("q", b, 1)
