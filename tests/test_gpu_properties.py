@@ -265,3 +265,55 @@ def test_mixed_sources_random_stream(dev, r, max_rows, borrow, kinds, final):
                                      momentum_buf=buf, momentum_init=True))
     same(cloud.cpu().numpy(), st_.cloud)
     same(buf.cpu().numpy(), st_.buf)
+
+
+@st.composite
+def ref_rounds(draw):
+    """A bf16 / fp16 / fp64 key: K rows of P values (normal, huge, tiny,
+    signed zeros, infinities), Python int / float weights (negative and zero
+    included), and a max_rows that drains in pieces."""
+    dtype = draw(st.sampled_from(["bfloat16", "float16", "float64"]))
+    K = draw(st.integers(1, 24))
+    P = draw(st.integers(1, 3000))
+    scale = draw(st.sampled_from([1e-3, 1.0, 300.0, 6e4]))
+    special = draw(st.booleans())
+    seed = draw(st.integers(0, 2 ** 31 - 1))
+    w = draw(st.lists(st.one_of(st.integers(-50, 600), st.floats(-4.0, 4.0, width=32)),
+                      min_size=K, max_size=K))
+    max_rows = draw(st.integers(1, 30))
+    return dtype, K, P, scale, special, seed, w, max_rows
+
+
+@SETTINGS
+@given(ref_rounds())
+def test_generic_kernel_matches_reference_arithmetic(dev, case):
+    """fedagg_reduce_rows_ref through the drop-in (HIP values, drained every
+    max_rows rows) against the reference's own CPU arithmetic on the same
+    values: bit for bit, NaNs compared as NaN (their sign / payload comes from
+    each device's arithmetic; bf16 stores one canonical NaN on both)."""
+    from fedsim_amd.utils import SerialAggregator
+    from oracle.reference_loop import ReferenceSerialAggregator
+
+    dtype, K, P, scale, special, seed, w, max_rows = case
+    dt = getattr(torch, dtype)
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(K, P, generator=g, dtype=torch.float64) * scale
+    if special:
+        idx = torch.randint(0, K * P, (max(1, K * P // 50),), generator=g)
+        vals = torch.tensor([0.0, -0.0, float("inf"), -float("inf"), 1e-42, 7e4])
+        X.view(-1)[idx] = vals[torch.randint(0, len(vals), idx.shape, generator=g)].double()
+    X = X.to(dt)
+    agg, ref_agg = SerialAggregator(max_rows=max_rows), ReferenceSerialAggregator()
+    for k in range(K):
+        agg.add("p", X[k].to(dev), w[k])
+        ref_agg.add("p", X[k], w[k])
+    for got, exp in ((agg.get_sum("p"), ref_agg.get_sum("p")), (agg.pop("p"), ref_agg.pop("p"))):
+        got = got.cpu()
+        assert got.dtype == exp.dtype and got.shape == exp.shape
+        nan_g, nan_e = torch.isnan(got), torch.isnan(exp)
+        assert torch.equal(nan_g, nan_e)
+        if dt == torch.bfloat16:  # one canonical NaN: the bits agree everywhere
+            assert torch.equal(got.view(torch.int16), exp.view(torch.int16))
+        else:
+            ib = torch.int16 if dt == torch.float16 else torch.int64
+            assert torch.equal(got[~nan_g].view(ib), exp[~nan_e].view(ib))
