@@ -3084,9 +3084,11 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 // ---------------------------------------------------------------------------
 // up: a stored element in the opmath type; rnd: an opmath value rounded to
 // the dtype, kept in the opmath type; store: the dtype's bits of an already
-// rounded value, a NaN as ATen's conversion writes it.  A NaN anywhere in a
-// column's chain stays NaN to the end, so the hardware conversions (RNE,
+// rounded value, a NaN as c10's scalar conversion writes it.  A NaN anywhere
+// in a column's chain stays NaN to the end, so the hardware conversions (RNE,
 // denormals kept) round every step and only the stored NaN is canonicalised.
+// (NaN bits are not pinned by the reference: ATen's AVX-512 bf16 conversion
+// writes 0xFFFF where its scalar one writes 0x7FC0.)
 struct RefBf16 {  // storage: the bf16 bits; opmath float
   using T = uint16_t;
   using OP = float;

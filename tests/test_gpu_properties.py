@@ -289,8 +289,9 @@ def ref_rounds(draw):
 def test_generic_kernel_matches_reference_arithmetic(dev, case):
     """fedagg_reduce_rows_ref through the drop-in (HIP values, drained every
     max_rows rows) against the reference's own CPU arithmetic on the same
-    values: bit for bit, NaNs compared as NaN (their sign / payload comes from
-    each device's arithmetic; bf16 stores one canonical NaN on both)."""
+    values: bit for bit, NaNs compared as NaN (inf * 0, inf - inf: their bits
+    are not pinned even within ATen -- its scalar bf16 conversion writes
+    0x7FC0, its AVX-512 one 0xFFFF)."""
     from fedsim_amd.utils import SerialAggregator
     from oracle.reference_loop import ReferenceSerialAggregator
 
@@ -312,8 +313,5 @@ def test_generic_kernel_matches_reference_arithmetic(dev, case):
         assert got.dtype == exp.dtype and got.shape == exp.shape
         nan_g, nan_e = torch.isnan(got), torch.isnan(exp)
         assert torch.equal(nan_g, nan_e)
-        if dt == torch.bfloat16:  # one canonical NaN: the bits agree everywhere
-            assert torch.equal(got.view(torch.int16), exp.view(torch.int16))
-        else:
-            ib = torch.int16 if dt == torch.float16 else torch.int64
-            assert torch.equal(got[~nan_g].view(ib), exp[~nan_e].view(ib))
+        ib = torch.int64 if dt == torch.float64 else torch.int16
+        assert torch.equal(got[~nan_g].view(ib), exp[~nan_e].view(ib))
