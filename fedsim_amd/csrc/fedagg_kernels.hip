@@ -3124,9 +3124,13 @@ struct RefF64 {
   static __device__ __forceinline__ double store(double v) { return v; }
 };
 
-// One lane: VW consecutive columns [c, c + VW) of every row, U rows' loads in
-// flight; columns from c_lo.  Row pointers and weights are wave-uniform.
-template <class R, int VW, int U>
+// One wave: a tile of NV * 64 consecutive VW-column vectors (a workgroup's
+// four waves: four consecutive tiles), every row; one lane: NV vectors 64
+// apart, so each load instruction reads 64 * VW consecutive elements of one
+// row; U rows' loads in flight; columns from c_lo.  Row pointers and weights
+// are wave-uniform.  Lanes past the last vector load the last one (in
+// bounds) and store nothing.
+template <class R, int VW, int U, int NV>
 __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* const* __restrict__ rows,
                                                          const typename R::OP* __restrict__ w,
                                                          int64_t B, int64_t c_lo, int64_t P,
@@ -3136,74 +3140,130 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
   using OP = typename R::OP;
   using V = T __attribute__((ext_vector_type(VW)));
   using GV = const __attribute__((address_space(1))) V;  // global loads, not flat
+  constexpr int kWaves = 256 / 64;
   const int64_t nvec = (P - c_lo) / VW;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec;
-       i += stride) {
-    const int64_t c = c_lo + i * VW;
-    OP s[VW];
+  const int64_t ntiles = (nvec + 64 * NV - 1) / (64 * NV);
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWaves;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6); t < ntiles;
+       t += nwaves) {
+    int64_t c[NV];
+    bool live[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int64_t i = t * (64 * NV) + v * 64 + lane;
+      live[v] = i < nvec;
+      c[v] = c_lo + (live[v] ? i : nvec - 1) * VW;
+    }
+    OP s[NV][VW];
     int64_t k = 0;
     if (init) {
-      const V x = *(GV*)(rows[0] + c);
       const OP w0 = w[0];
 #pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        const OP t = R::rnd(R::up(x[j]) * w0);
-        s[j] = R::rnd(t + OP(0));
+      for (int v = 0; v < NV; ++v) {
+        const V x = *(GV*)(rows[0] + c[v]);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const OP p = R::rnd(R::up(x[j]) * w0);
+          s[v][j] = R::rnd(p + OP(0));
+        }
       }
       k = 1;
     } else {
-      const V a = *reinterpret_cast<const V*>(acc_in + c);
 #pragma unroll
-      for (int j = 0; j < VW; ++j) s[j] = R::up(a[j]);
+      for (int v = 0; v < NV; ++v) {
+        const V a = *(GV*)(acc_in + c[v]);
+#pragma unroll
+        for (int j = 0; j < VW; ++j) s[v][j] = R::up(a[j]);
+      }
     }
     for (; k + U <= B; k += U) {
-      V x[U];
+      V x[U][NV];
 #pragma unroll
-      for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load((GV*)(rows[k + u] + c));
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) x[u][v] = __builtin_nontemporal_load((GV*)(rows[k + u] + c[v]));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const OP wk = w[k + u];
 #pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          const OP t = R::rnd(R::up(x[u][j]) * wk);
-          s[j] = R::rnd(s[j] + t);
-        }
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const OP p = R::rnd(R::up(x[u][v][j]) * wk);
+            s[v][j] = R::rnd(s[v][j] + p);
+          }
       }
     }
     for (; k < B; ++k) {
-      const V x = __builtin_nontemporal_load((GV*)(rows[k] + c));
       const OP wk = w[k];
 #pragma unroll
-      for (int j = 0; j < VW; ++j) {
-        const OP t = R::rnd(R::up(x[j]) * wk);
-        s[j] = R::rnd(s[j] + t);
+      for (int v = 0; v < NV; ++v) {
+        const V x = __builtin_nontemporal_load((GV*)(rows[k] + c[v]));
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const OP p = R::rnd(R::up(x[j]) * wk);
+          s[v][j] = R::rnd(s[v][j] + p);
+        }
       }
     }
-    V o;
 #pragma unroll
-    for (int j = 0; j < VW; ++j) o[j] = R::store(s[j]);
-    *reinterpret_cast<V*>(out + c) = o;
+    for (int v = 0; v < NV; ++v) {
+      if (!live[v]) continue;
+      V o;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) o[j] = R::store(s[v][j]);
+      *reinterpret_cast<V*>(out + c[v]) = o;
+    }
   }
 }
 
-template <class R, int VW>
-hipError_t launch_rows_ref(const void* const* rows, const void* w, int64_t B, int64_t P,
-                           const void* acc_in, void* out, bool init, bool vec, hipStream_t st) {
+// Workgroups: one per four tiles (the dispatcher balances them; past 2^30
+// workgroups the waves stride over the rest).
+inline int64_t rows_ref_blocks(int64_t nvec, int nv) {
+  const int64_t tiles = (nvec + 64 * nv - 1) / (64 * nv);
+  const int64_t g = (tiles + 3) / 4;
+  return g < 1 ? 1 : (g < (int64_t(1) << 30) ? g : (int64_t(1) << 30));
+}
+
+template <class R, int VW, int U, int NV>
+hipError_t launch_rows_ref_tile(const void* const* rows, const void* w, int64_t B, int64_t P,
+                                const void* acc_in, void* out, bool init, int64_t body,
+                                hipStream_t st) {
   using T = typename R::T;
   using OP = typename R::OP;
   auto rt = reinterpret_cast<const T* const*>(rows);
   auto wt = static_cast<const OP*>(w);
   auto ai = static_cast<const T*>(acc_in);
   auto ot = static_cast<T*>(out);
-  const int64_t body = vec ? P / VW * VW : 0;
   if (body > 0)
-    hipLaunchKernelGGL((k_reduce_rows_ref<R, VW, 8>), dim3(elementwise_grid(body / VW)),
+    hipLaunchKernelGGL((k_reduce_rows_ref<R, VW, U, NV>), dim3(static_cast<uint32_t>(rows_ref_blocks(body / VW, NV))),
                        dim3(kBlock), 0, st, rt, wt, B, int64_t(0), body, ai, ot, init ? 1 : 0);
   if (body < P)  // columns past the last full vector (or every column: unaligned rows)
-    hipLaunchKernelGGL((k_reduce_rows_ref<R, 1, 8>), dim3(elementwise_grid(P - body)),
+    hipLaunchKernelGGL((k_reduce_rows_ref<R, 1, U, NV>), dim3(static_cast<uint32_t>(rows_ref_blocks(P - body, NV))),
                        dim3(kBlock), 0, st, rt, wt, B, body, P, ai, ot, init ? 1 : 0);
   return hipGetLastError();
+}
+
+// Tile ladder, widest first.  A wave reading NV KiB of one row per load
+// batch (16-B lanes) instead of 1 KiB keeps the K row streams' DRAM pages
+// open longer: at K=200 x 50 MB rows the generic kernel went 5.6-5.9 ->
+// 6.3-6.7 TB/s for U x NV = 2 x 8 (bf16), 4 x 8 (fp16) and 4 x 12 (fp64),
+// bitwise the same sums (profiles/r05m*, r05n; bf16 at 4 x 8 spills).  A wide tile is taken only while the launch
+// still has kRefMinBlocks workgroups (2 per CU): below that, the narrow tile
+// (8 rows of 1 KiB in flight) fills the chip.
+constexpr int64_t kRefMinBlocks = 512;
+
+template <class R, int VW, int U, int NV>
+hipError_t launch_rows_ref(const void* const* rows, const void* w, int64_t B, int64_t P,
+                           const void* acc_in, void* out, bool init, bool vec, hipStream_t st) {
+  const int64_t body = vec ? P / VW * VW : 0;
+  const int64_t nvec = body ? body / VW : P;
+  if (rows_ref_blocks(nvec, NV) >= kRefMinBlocks)
+    return launch_rows_ref_tile<R, VW, U, NV>(rows, w, B, P, acc_in, out, init, body, st);
+  if (rows_ref_blocks(nvec, 4) >= kRefMinBlocks)
+    return launch_rows_ref_tile<R, VW, 4, 4>(rows, w, B, P, acc_in, out, init, body, st);
+  return launch_rows_ref_tile<R, VW, 8, 1>(rows, w, B, P, acc_in, out, init, body, st);
 }
 
 }  // namespace
@@ -3753,11 +3813,11 @@ int fedagg_reduce_rows_ref(int dtype, const void* const* rows, const void* w, in
   const bool vec = !(flags & FEDAGG_SCALAR) && aligned16(out) && (init || aligned16(acc_in));
   switch (dtype) {
     case FEDAGG_DTYPE_BF16:
-      return static_cast<int>(launch_rows_ref<RefBf16, 8>(rows, w, B, P, acc_in, out, init, vec, st));
+      return static_cast<int>(launch_rows_ref<RefBf16, 8, 2, 8>(rows, w, B, P, acc_in, out, init, vec, st));
     case FEDAGG_DTYPE_F16:
-      return static_cast<int>(launch_rows_ref<RefF16, 8>(rows, w, B, P, acc_in, out, init, vec, st));
+      return static_cast<int>(launch_rows_ref<RefF16, 8, 4, 8>(rows, w, B, P, acc_in, out, init, vec, st));
     case FEDAGG_DTYPE_F64:
-      return static_cast<int>(launch_rows_ref<RefF64, 2>(rows, w, B, P, acc_in, out, init, vec, st));
+      return static_cast<int>(launch_rows_ref<RefF64, 2, 4, 12>(rows, w, B, P, acc_in, out, init, vec, st));
     default:
       return FEDAGG_EINVAL;
   }
