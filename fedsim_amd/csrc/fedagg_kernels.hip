@@ -1249,6 +1249,8 @@ int max_cols_per_lane(int64_t P, std::initializer_list<const void*> ptrs) {
 // Borrowed rows (pointer table) with two columns per lane read two pieces per
 // lane from P >= kRowsPiecesP on, with at most kRowsPiecesU rows in flight
 // (profiles/r01cf/).
+// (Round 5: 4 / 8 / 16 pieces with 2..8 rows in flight measured no faster at
+// 1000 x 25 M / 12.5 M, profiles/r05p/.)
 constexpr int kRowsPieces = 2;
 constexpr int kRowsPiecesU = 8;
 constexpr int64_t kRowsPiecesP = int64_t(1) << 22;
@@ -3089,40 +3091,149 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 // denormals kept) round every step and only the stored NaN is canonicalised.
 // (NaN bits are not pinned by the reference: ATen's AVX-512 bf16 conversion
 // writes 0xFFFF where its scalar one writes 0x7FC0.)
-struct RefBf16 {  // storage: the bf16 bits; opmath float
-  using T = uint16_t;
-  using OP = float;
+// The kernel's hooks, per 16-B (or narrower) vector of VW elements: the
+// accumulator type ACC, first (s = rnd(rnd(x * w) + 0)), madd (s = rnd(s +
+// rnd(x * w))), load (s from a stored running sum) and store.  RefEach spells
+// them element by element from up / rnd / store_one.
+template <class D, class T_, class OP_>
+struct RefEach {
+  using T = T_;
+  using OP = OP_;
+  using ACC = OP_;
+  template <int VW> using V = T_ __attribute__((ext_vector_type(VW)));
+  template <int VW>
+  static __device__ __forceinline__ void first(OP_ (&s)[VW], const V<VW>& x, OP_ w) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) s[j] = D::rnd(D::rnd(D::up(x[j]) * w) + OP_(0));
+  }
+  template <int VW>
+  static __device__ __forceinline__ void madd(OP_ (&s)[VW], const V<VW>& x, OP_ w) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) s[j] = D::rnd(s[j] + D::rnd(D::up(x[j]) * w));
+  }
+  template <int VW>
+  static __device__ __forceinline__ void load(OP_ (&s)[VW], const V<VW>& a) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) s[j] = D::up(a[j]);
+  }
+  template <int VW>
+  static __device__ __forceinline__ V<VW> store(const OP_ (&s)[VW]) {
+    V<VW> o;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) o[j] = D::store_one(s[j]);
+    return o;
+  }
+};
+
+struct RefBf16 : RefEach<RefBf16, uint16_t, float> {  // storage: the bf16 bits; opmath float
   static __device__ __forceinline__ float up(uint16_t u) {
     return __builtin_bit_cast(float, static_cast<uint32_t>(u) << 16);
   }
   static __device__ __forceinline__ float rnd(float x) {  // v_cvt_pk_bf16_f32
     return up(__builtin_bit_cast(uint16_t, static_cast<__bf16>(x)));
   }
-  static __device__ __forceinline__ uint16_t store(float x) {  // c10::BFloat16: NaN -> 0x7FC0
+  static __device__ __forceinline__ uint16_t store_one(float x) {  // c10::BFloat16: NaN -> 0x7FC0
     return x != x ? uint16_t(0x7FC0) : __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));
   }
 };
+
+// fp16: the running sum stays in f16 registers and is added with v_pk_add_f16:
+// for two f16 values fl16(fl32(s + p)) == fl16(s + p) (double rounding is
+// innocuous for a sum when 24 >= 2 * 11 + 2; subnormal sums are exact in
+// both), so the native add IS ATen's float-opmath add.  The product is not
+// (w is an f32 weight): fl16(fl32(x * w)) keeps its two roundings -- the
+// f32 products pass an empty register barrier before the conversion, else
+// the compiler folds fptrunc(x * w) into v_fma_mixlo_f16, one rounding of
+// the exact product, which differs on a tie of the first (3 of 8.4 M columns
+// with w = 0.37, tests/test_generic_keys.py test_reference_kernel_tile_rungs).
 struct RefF16 {  // storage: the fp16 bits; opmath float
   using T = uint16_t;
   using OP = float;
+  using ACC = _Float16;
+  template <int VW> using V = uint16_t __attribute__((ext_vector_type(VW)));
+  using f2 = float __attribute__((ext_vector_type(2)));
+  using h2 = _Float16 __attribute__((ext_vector_type(2)));
   static __device__ __forceinline__ float up(uint16_t u) {
     return static_cast<float>(__builtin_bit_cast(_Float16, u));
   }
-  static __device__ __forceinline__ float rnd(float x) {  // v_cvt_f16_f32
-    return static_cast<float>(static_cast<_Float16>(x));
+  template <int VW>
+  static __device__ __forceinline__ void prod(_Float16 (&p)[VW], const V<VW>& x, float w) {
+    if constexpr (VW % 2 == 0) {
+#pragma unroll
+      for (int j = 0; j < VW; j += 2) {
+        f2 q = f2{up(x[j]), up(x[j + 1])} * w;  // v_pk_mul_f32
+        asm("" : "+v"(q));
+        const h2 r = __builtin_convertvector(q, h2);  // v_cvt_pk_f16_f32 (RNE)
+        p[j] = r.x;
+        p[j + 1] = r.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        float q = up(x[j]) * w;
+        asm("" : "+v"(q));
+        p[j] = static_cast<_Float16>(q);
+      }
+    }
   }
-  static __device__ __forceinline__ uint16_t store(float x) {  // c10::Half: NaN -> sign | 0x7E00
-    if (x != x) return static_cast<uint16_t>((__builtin_bit_cast(uint32_t, x) >> 16) & 0x8000u) | 0x7E00u;
-    return __builtin_bit_cast(uint16_t, static_cast<_Float16>(x));
+  template <int VW>
+  static __device__ __forceinline__ void first(_Float16 (&s)[VW], const V<VW>& x, float w) {
+    _Float16 p[VW];
+    prod<VW>(p, x, w);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) s[j] = p[j] + static_cast<_Float16>(0.f);  // -0 + 0 = +0
+  }
+  template <int VW>
+  static __device__ __forceinline__ void madd(_Float16 (&s)[VW], const V<VW>& x, float w) {
+    _Float16 p[VW];
+    prod<VW>(p, x, w);
+    if constexpr (VW % 2 == 0) {
+#pragma unroll
+      for (int j = 0; j < VW; j += 2) {
+        const h2 r = h2{s[j], s[j + 1]} + h2{p[j], p[j + 1]};  // v_pk_add_f16
+        s[j] = r.x;
+        s[j + 1] = r.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VW; ++j) s[j] = s[j] + p[j];
+    }
+  }
+  template <int VW>
+  static __device__ __forceinline__ void load(_Float16 (&s)[VW], const V<VW>& a) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      // through a scalar: __builtin_bit_cast of the vector element a[j] itself
+      // read element 0 for every j (clang, ROCm 7.2)
+      const uint16_t u = a[j];
+      s[j] = __builtin_bit_cast(_Float16, u);
+    }
+  }
+  template <int VW>
+  static __device__ __forceinline__ V<VW> store(const _Float16 (&s)[VW]) {  // c10::Half: NaN -> sign | 0x7E00
+    V<VW> o;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const uint16_t b = __builtin_bit_cast(uint16_t, s[j]);
+      o[j] = s[j] != s[j] ? static_cast<uint16_t>((b & 0x8000u) | 0x7E00u) : b;
+    }
+    return o;
   }
 };
-struct RefF64 {
-  using T = double;
-  using OP = double;
+
+struct RefF64 : RefEach<RefF64, double, double> {
   static __device__ __forceinline__ double up(double v) { return v; }
   static __device__ __forceinline__ double rnd(double v) { return v; }
-  static __device__ __forceinline__ double store(double v) { return v; }
+  static __device__ __forceinline__ double store_one(double v) { return v; }
 };
+
+#ifdef FEDAGG_EXP_F32REF
+struct RefF32 : RefEach<RefF32, float, float> {  // experiment: the fp32 sum through this kernel
+  static __device__ __forceinline__ float up(float v) { return v; }
+  static __device__ __forceinline__ float rnd(float v) { return v; }
+  static __device__ __forceinline__ float store_one(float v) { return v; }
+};
+#endif
 
 // One wave: a tile of NV * 64 consecutive VW-column vectors (a workgroup's
 // four waves: four consecutive tiles), every row; one lane: NV vectors 64
@@ -3138,6 +3249,7 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
                                                          typename R::T* __restrict__ out, int init) {
   using T = typename R::T;
   using OP = typename R::OP;
+  using ACC = typename R::ACC;
   using V = T __attribute__((ext_vector_type(VW)));
   using GV = const __attribute__((address_space(1))) V;  // global loads, not flat
   constexpr int kWaves = 256 / 64;
@@ -3155,26 +3267,21 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
       live[v] = i < nvec;
       c[v] = c_lo + (live[v] ? i : nvec - 1) * VW;
     }
-    OP s[NV][VW];
+    ACC s[NV][VW];
     int64_t k = 0;
     if (init) {
       const OP w0 = w[0];
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const V x = *(GV*)(rows[0] + c[v]);
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          const OP p = R::rnd(R::up(x[j]) * w0);
-          s[v][j] = R::rnd(p + OP(0));
-        }
+        R::template first<VW>(s[v], x, w0);
       }
       k = 1;
     } else {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const V a = *(GV*)(acc_in + c[v]);
-#pragma unroll
-        for (int j = 0; j < VW; ++j) s[v][j] = R::up(a[j]);
+        R::template load<VW>(s[v], a);
       }
     }
     for (; k + U <= B; k += U) {
@@ -3187,12 +3294,7 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
       for (int u = 0; u < U; ++u) {
         const OP wk = w[k + u];
 #pragma unroll
-        for (int v = 0; v < NV; ++v)
-#pragma unroll
-          for (int j = 0; j < VW; ++j) {
-            const OP p = R::rnd(R::up(x[u][v][j]) * wk);
-            s[v][j] = R::rnd(s[v][j] + p);
-          }
+        for (int v = 0; v < NV; ++v) R::template madd<VW>(s[v], x[u][v], wk);
       }
     }
     for (; k < B; ++k) {
@@ -3200,21 +3302,12 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const V x = __builtin_nontemporal_load((GV*)(rows[k] + c[v]));
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-          const OP p = R::rnd(R::up(x[j]) * wk);
-          s[v][j] = R::rnd(s[v][j] + p);
-        }
+        R::template madd<VW>(s[v], x, wk);
       }
     }
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      if (!live[v]) continue;
-      V o;
-#pragma unroll
-      for (int j = 0; j < VW; ++j) o[j] = R::store(s[v][j]);
-      *reinterpret_cast<V*>(out + c[v]) = o;
-    }
+    for (int v = 0; v < NV; ++v)
+      if (live[v]) *reinterpret_cast<V*>(out + c[v]) = R::template store<VW>(s[v]);
   }
 }
 
@@ -3818,6 +3911,15 @@ int fedagg_reduce_rows_ref(int dtype, const void* const* rows, const void* w, in
       return static_cast<int>(launch_rows_ref<RefF16, 8, 4, 8>(rows, w, B, P, acc_in, out, init, vec, st));
     case FEDAGG_DTYPE_F64:
       return static_cast<int>(launch_rows_ref<RefF64, 2, 4, 12>(rows, w, B, P, acc_in, out, init, vec, st));
+#ifdef FEDAGG_EXP_F32REF
+    case 4: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 2, 8>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+    case 5: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 4, 8>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+    case 6: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 4, 4>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+    case 7: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 8, 4>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+    case 8: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 4, 12>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+    case 9: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 8, 1>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+    case 10: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 8, 8>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
+#endif
     default:
       return FEDAGG_EINVAL;
   }

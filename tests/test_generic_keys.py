@@ -188,3 +188,51 @@ def test_hbm_reference_arithmetic_kernel(dtype, borrow, max_rows):
     got = agg.pop("p")
     assert got.device == dev and got.dtype == dt
     assert G.encode(got) == G.encode(ref.pop("p"))
+
+
+# fedagg_reduce_rows_ref's tile ladder (fedagg_kernels.hip launch_rows_ref):
+# per dtype the wide tile from ~8.4 M (bf16 / fp16) or ~3.2 M (fp64) columns,
+# the 4 x 4 tile from ~4.2 M / ~1.05 M, the narrow one below; sizes with a
+# partial last tile and a few columns past the last 16-B vector.
+_RUNGS = {
+    "bfloat16": (8_400_003, 4_200_001, 1_001),
+    "float16": (8_400_005, 4_200_007, 999),
+    "float64": (3_200_001, 1_100_003, 997),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", sorted(_RUNGS))
+@pytest.mark.parametrize("rung", [0, 1, 2], ids=["wide", "mid", "narrow"])
+@pytest.mark.parametrize("aligned", [True, False], ids=["vec", "scalar"])
+def test_reference_kernel_tile_rungs(dtype, rung, aligned):
+    """Every tile of the generic kernel, vector body + tail and the all-scalar
+    path (a row off 16-B alignment): bitwise the reference's CPU arithmetic;
+    a chained call (the running sum as acc_in) equals one call over all rows."""
+    from fedsim_amd import ops
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    K, P = 11, _RUNGS[dtype][rung]
+    g = torch.Generator().manual_seed(17 + rung)
+    X = [(torch.randn(P, generator=g, dtype=torch.float32) * 0.5).to(dt) for _ in range(K)]
+    w = [int(v) for v in torch.randint(1, 600, (K,), generator=g)]
+    w[2] = 0.37
+    ref = ReferenceSerialAggregator()
+    for k in range(K):
+        ref.add("p", X[k], w[k])
+    want = ref.get_sum("p")
+    rows = [x.to(dev) for x in X]
+    if not aligned:
+        big = torch.empty(P + 1, dtype=dt, device=dev)
+        big[1:].copy_(X[5])
+        rows[5] = big[1:]
+    out = torch.empty(P, dtype=dt, device=dev)
+    ops.reduce_rows_ref(rows, w, out)
+    ib = torch.int64 if dt == torch.float64 else torch.int16
+    assert torch.equal(out.cpu().view(ib), want.view(ib))
+    head = torch.empty(P, dtype=dt, device=dev)
+    ops.reduce_rows_ref(rows[:6], w[:6], head)
+    tail = torch.empty(P, dtype=dt, device=dev)
+    ops.reduce_rows_ref(rows[6:], w[6:], tail, acc_in=head)
+    assert torch.equal(tail.view(ib), out.view(ib))

@@ -1,5 +1,6 @@
 """A/B of libfedagg BUILD variants of fedagg_reduce_rows_ref (the generic
-keys' kernel): bf16 / fp16 / fp64 rounds of K handed-over client rows (K
+keys' kernel; float32 in --dtypes: fedagg_reduce_rows_f32, the fp32 kernel's
+borrowed-row path): bf16 / fp16 / fp64 rounds of K handed-over client rows (K
 separate 50 MB allocations), each library its own ctypes handle, run
 interleaved in one process, every output compared bitwise with the first
 library's.  HIP events around each launch; GB/s of client bytes read.
@@ -49,6 +50,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--dtypes", default="bfloat16,float16,float64")
+    ap.add_argument("--f32-codes", default="",
+                    help="float32: also run fedagg_reduce_rows_ref with these dtype codes "
+                         "(builds with -DFEDAGG_EXP_F32REF), separated by :")
     a = ap.parse_args()
     if a.build:
         build(a.build[0], a.build[1:])
@@ -60,10 +64,13 @@ def main():
     libs = []
     for p in a.libs:
         lib = ctypes.CDLL(os.path.abspath(p), mode=ctypes.RTLD_LOCAL)
-        res, args = _native.SIGNATURES["fedagg_reduce_rows_ref"]
-        fn = lib.fedagg_reduce_rows_ref
-        fn.restype, fn.argtypes = res, args
-        libs.append((os.path.basename(p), fn))
+        fns = {}
+        for entry in ("fedagg_reduce_rows_ref", "fedagg_reduce_rows_f32"):
+            res, args = _native.SIGNATURES[entry]
+            fn = getattr(lib, entry)
+            fn.restype, fn.argtypes = res, args
+            fns[entry] = fn
+        libs.append((os.path.basename(p), fns))
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     codes = {torch.bfloat16: _native.FEDAGG_DTYPE_BF16, torch.float16: _native.FEDAGG_DTYPE_F16,
@@ -78,23 +85,36 @@ def main():
         wdt = torch.float64 if dt == torch.float64 else torch.float32
         w = torch.tensor([float(50 + (k * 37) % 551) for k in range(a.K)], dtype=wdt, device=dev)
         table = ops.row_table_from_ptrs([r.data_ptr() for r in rows], dev)
-        outs = [torch.empty(P, device=dev, dtype=dt) for _ in libs]
-        times = {n: [] for n, _ in libs}
+        variants = []
+        for n, fns in libs:
+            if dt == torch.float32:
+                variants.append((n, lambda out, f=fns["fedagg_reduce_rows_f32"]: f(
+                    table.data_ptr(), w.data_ptr(), a.K, P, None, out.data_ptr(), 0.0,
+                    _native.FEDAGG_INIT, ops._stream_ptr(dev))))
+                for code in [int(c) for c in a.f32_codes.replace(":", ",").split(",") if c]:
+                    variants.append((f"{n}#{code}", lambda out, f=fns["fedagg_reduce_rows_ref"], c=code: f(
+                        c, table.data_ptr(), w.data_ptr(), a.K, P, None, out.data_ptr(),
+                        _native.FEDAGG_INIT, ops._stream_ptr(dev))))
+            else:
+                variants.append((n, lambda out, f=fns["fedagg_reduce_rows_ref"]: f(
+                    codes[dt], table.data_ptr(), w.data_ptr(), a.K, P, None, out.data_ptr(),
+                    _native.FEDAGG_INIT, ops._stream_ptr(dev))))
+        outs = [torch.empty(P, device=dev, dtype=dt) for _ in variants]
+        times = {n: [] for n, _ in variants}
         for _ in range(a.rounds):
-            for (n, fn), out in zip(libs, outs):
+            for (n, fn), out in zip(variants, outs):
                 for it in range(a.iters + 1):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(st)
-                    rc = fn(codes[dt], table.data_ptr(), w.data_ptr(), a.K, P, None, out.data_ptr(),
-                            _native.FEDAGG_INIT, ops._stream_ptr(dev))
+                    rc = fn(out)
                     e1.record(st)
                     e1.synchronize()
                     if rc != 0:
                         raise RuntimeError(f"{n}: rc {rc}")
                     if it:
                         times[n].append(e0.elapsed_time(e1))
-        ib = torch.int64 if dt == torch.float64 else torch.int16
-        for (n, _), out in zip(libs, outs):
+        ib = {torch.float64: torch.int64, torch.float32: torch.int32}.get(dt, torch.int16)
+        for (n, _), out in zip(variants, outs):
             med = statistics.median(times[n])
             print(json.dumps(dict(lib=n, dtype=name, K=a.K, P=P, ms_median=round(med, 4),
                                   ms_best=round(min(times[n]), 4),
