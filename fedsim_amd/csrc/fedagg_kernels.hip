@@ -3100,6 +3100,7 @@ struct RefEach {
   using T = T_;
   using OP = OP_;
   using ACC = OP_;
+  static constexpr bool kFinalize = false;  // divide by W32 before the store
   template <int VW> using V = T_ __attribute__((ext_vector_type(VW)));
   template <int VW>
   static __device__ __forceinline__ void first(OP_ (&s)[VW], const V<VW>& x, OP_ w) {
@@ -3150,6 +3151,7 @@ struct RefF16 {  // storage: the fp16 bits; opmath float
   using T = uint16_t;
   using OP = float;
   using ACC = _Float16;
+  static constexpr bool kFinalize = false;
   template <int VW> using V = uint16_t __attribute__((ext_vector_type(VW)));
   using f2 = float __attribute__((ext_vector_type(2)));
   using h2 = _Float16 __attribute__((ext_vector_type(2)));
@@ -3227,13 +3229,15 @@ struct RefF64 : RefEach<RefF64, double, double> {
   static __device__ __forceinline__ double store_one(double v) { return v; }
 };
 
-#ifdef FEDAGG_EXP_F32REF
-struct RefF32 : RefEach<RefF32, float, float> {  // experiment: the fp32 sum through this kernel
+// fp32 client rows (fedagg_reduce_rows_f32's borrowed rows, round 5): the
+// exact-mode sum acc = fl32(acc + fl32(x * w)) from +0, and FEDAGG_FINALIZE's
+// IEEE division by fl32(W) -- the narrow kernel's arithmetic, bit for bit.
+struct RefF32 : RefEach<RefF32, float, float> {
+  static constexpr bool kFinalize = true;
   static __device__ __forceinline__ float up(float v) { return v; }
   static __device__ __forceinline__ float rnd(float v) { return v; }
   static __device__ __forceinline__ float store_one(float v) { return v; }
 };
-#endif
 
 // One wave: a tile of NV * 64 consecutive VW-column vectors (a workgroup's
 // four waves: four consecutive tiles), every row; one lane: NV vectors 64
@@ -3246,7 +3250,8 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
                                                          const typename R::OP* __restrict__ w,
                                                          int64_t B, int64_t c_lo, int64_t P,
                                                          const typename R::T* __restrict__ acc_in,
-                                                         typename R::T* __restrict__ out, int init) {
+                                                         typename R::T* __restrict__ out, int init,
+                                                         typename R::OP W, int fin) {
   using T = typename R::T;
   using OP = typename R::OP;
   using ACC = typename R::ACC;
@@ -3305,6 +3310,14 @@ __global__ __launch_bounds__(256) void k_reduce_rows_ref(const typename R::T* co
         R::template madd<VW>(s[v], x, wk);
       }
     }
+    if constexpr (R::kFinalize) {
+      if (fin) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+          for (int j = 0; j < VW; ++j) s[v][j] = s[v][j] / W;
+      }
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v)
       if (live[v]) *reinterpret_cast<V*>(out + c[v]) = R::template store<VW>(s[v]);
@@ -3322,7 +3335,7 @@ inline int64_t rows_ref_blocks(int64_t nvec, int nv) {
 template <class R, int VW, int U, int NV>
 hipError_t launch_rows_ref_tile(const void* const* rows, const void* w, int64_t B, int64_t P,
                                 const void* acc_in, void* out, bool init, int64_t body,
-                                hipStream_t st) {
+                                hipStream_t st, typename R::OP W = 0, bool fin = false) {
   using T = typename R::T;
   using OP = typename R::OP;
   auto rt = reinterpret_cast<const T* const*>(rows);
@@ -3331,10 +3344,12 @@ hipError_t launch_rows_ref_tile(const void* const* rows, const void* w, int64_t 
   auto ot = static_cast<T*>(out);
   if (body > 0)
     hipLaunchKernelGGL((k_reduce_rows_ref<R, VW, U, NV>), dim3(static_cast<uint32_t>(rows_ref_blocks(body / VW, NV))),
-                       dim3(kBlock), 0, st, rt, wt, B, int64_t(0), body, ai, ot, init ? 1 : 0);
+                       dim3(kBlock), 0, st, rt, wt, B, int64_t(0), body, ai, ot, init ? 1 : 0, W,
+                       fin ? 1 : 0);
   if (body < P)  // columns past the last full vector (or every column: unaligned rows)
     hipLaunchKernelGGL((k_reduce_rows_ref<R, 1, U, NV>), dim3(static_cast<uint32_t>(rows_ref_blocks(P - body, NV))),
-                       dim3(kBlock), 0, st, rt, wt, B, body, P, ai, ot, init ? 1 : 0);
+                       dim3(kBlock), 0, st, rt, wt, B, body, P, ai, ot, init ? 1 : 0, W,
+                       fin ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -3434,6 +3449,21 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
   if (const int S = fast_split(flags, P))
     return static_cast<int>(launch_splitk(NarrowTable{rows, table_row_bytes(P)}, S, w, B, P,
                                           acc_in, EpiStore{out}, W32, flags, s));
+  // 16-B rows with the default column mapping: wide per-row tiles
+  // (k_reduce_rows_ref<RefF32>, one wave = 8 or 4 KiB of each row per visit)
+  // while the launch keeps kRefMinBlocks workgroups -- 6.0-6.1 -> 6.5-6.7
+  // TB/s at 16-100 MB rows, bitwise the narrow kernel's sums (round 5,
+  // profiles/r05p/, r05u/).  A forced mapping keeps the narrow kernels.
+  if (B > 0 && vec_ok && max_vw == 4 && (flags & FEDAGG_MAP_MASK) == 0) {
+    const bool fin = (flags & FEDAGG_FINALIZE) != 0;
+    const auto rt = reinterpret_cast<const void* const*>(rows);
+    if (rows_ref_blocks(P / 4, 8) >= kRefMinBlocks)
+      return static_cast<int>(
+          launch_rows_ref_tile<RefF32, 4, 4, 8>(rt, w, B, P, acc_in, out, init, P, s, W32, fin));
+    if (rows_ref_blocks(P / 4, 4) >= kRefMinBlocks)
+      return static_cast<int>(
+          launch_rows_ref_tile<RefF32, 4, 8, 4>(rt, w, B, P, acc_in, out, init, P, s, W32, fin));
+  }
   const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
   if (vw)
     return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B, P,
@@ -3911,15 +3941,6 @@ int fedagg_reduce_rows_ref(int dtype, const void* const* rows, const void* w, in
       return static_cast<int>(launch_rows_ref<RefF16, 8, 4, 8>(rows, w, B, P, acc_in, out, init, vec, st));
     case FEDAGG_DTYPE_F64:
       return static_cast<int>(launch_rows_ref<RefF64, 2, 4, 12>(rows, w, B, P, acc_in, out, init, vec, st));
-#ifdef FEDAGG_EXP_F32REF
-    case 4: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 2, 8>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-    case 5: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 4, 8>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-    case 6: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 4, 4>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-    case 7: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 8, 4>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-    case 8: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 4, 12>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-    case 9: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 8, 1>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-    case 10: return static_cast<int>(launch_rows_ref_tile<RefF32, 4, 8, 8>(rows, w, B, P, acc_in, out, init, P / 4 * 4, st));
-#endif
     default:
       return FEDAGG_EINVAL;
   }
