@@ -4,7 +4,7 @@ then fedagg_server_step_f32 on the stored average), both with the same
 ServerStep operands and outputs, as SerialAggregator.pop_step issues them.
 Interleaved per round, bitwise-checked against each other.
 
-python tools/ab_fused_split.py [--K 1000] [--Ps 199210,1085668,...] [--algos fedavg,adabest]
+python tools/ab_fused_split.py [--K 1000[:K2...]] [--Ps 199210,1085668,...] [--algos fedavg,adabest]
 """
 import argparse
 import json
@@ -20,7 +20,7 @@ from fedsim_amd import ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--K", type=int, default=1000)
+    ap.add_argument("--K", default="1000", help="client counts, separated by : or ,")
     ap.add_argument("--Ps", default="199210,1085668,2097152,4194304,6250000,12500000,25000000")
     ap.add_argument("--algos", default="fedavg,adabest")
     ap.add_argument("--rounds", type=int, default=5)
@@ -28,10 +28,14 @@ def main():
                     help="rows: the borrowed path (fedagg_reduce_step_rows_f32 vs "
                          "fedagg_reduce_rows_f32 + fedagg_server_step_f32) over K separate tensors")
     a = ap.parse_args()
-    K = a.K
+    for K in [int(x) for x in a.K.replace(":", ",").split(",")]:
+        run(a, K)
+
+
+def run(a, K):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(7)
-    for P in [int(x) for x in a.Ps.split(",")]:
+    for P in [int(x) for x in a.Ps.replace(":", ",").split(",")]:
         C = ops.choose_block_cols(P)
         if a.layout == "rows":
             rows = [torch.empty(P, device=dev).normal_(0, 0.05, generator=g) for _ in range(K)]
