@@ -3075,7 +3075,8 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 // ---------------------------------------------------------------------------
 // The reference's arithmetic on bf16 / fp16 / fp64 client rows (the
 // dtype-generic SerialAggregator keys: aggregators.py:17-40 on such
-// tensors).  ATen computes ``value * weight`` and ``sum_v + new_v`` of
+// tensors), and on fp32 rows held in separate allocations (RefF32 below:
+// fedagg_reduce_rows_f32's wide-tile path).  ATen computes ``value * weight`` and ``sum_v + new_v`` of
 // reduced-precision tensors in float (its opmath type) and rounds each result
 // to the tensor's dtype; fp64 rounds each in double.  Per column, in arrival
 // order:
@@ -3085,7 +3086,7 @@ __global__ __launch_bounds__(256) void k_pad_lrn_maxpool_slide(const float* __re
 // No FMA (-ffp-contract=off): every product and sum rounds on its own.
 // ---------------------------------------------------------------------------
 // up: a stored element in the opmath type; rnd: an opmath value rounded to
-// the dtype, kept in the opmath type; store: the dtype's bits of an already
+// the dtype, kept in the opmath type; store_one: the dtype's bits of an already
 // rounded value, a NaN as c10's scalar conversion writes it.  A NaN anywhere
 // in a column's chain stays NaN to the end, so the hardware conversions (RNE,
 // denormals kept) round every step and only the stored NaN is canonicalised.
