@@ -315,3 +315,94 @@ def test_generic_kernel_matches_reference_arithmetic(dev, case):
         assert torch.equal(nan_g, nan_e)
         ib = torch.int64 if dt == torch.float64 else torch.int16
         assert torch.equal(got[~nan_g].view(ib), exp[~nan_e].view(ib))
+
+
+# The tile ladders of k_reduce_rows_ref (fedagg_kernels.hip launch_rows_ref
+# and fedagg_reduce_rows_f32): P ranges that select each tile.
+_REF_RUNGS = {
+    "bfloat16": [(1, 4_100_000), (4_190_000, 8_300_000), (8_380_000, 9_000_000)],
+    "float16": [(1, 4_100_000), (4_190_000, 8_300_000), (8_380_000, 9_000_000)],
+    "float64": [(1, 1_000_000), (1_050_000, 3_100_000), (3_150_000, 3_600_000)],
+}
+WIDE = settings(max_examples=24, deadline=None, derandomize=True,
+                suppress_health_check=[HealthCheck.too_slow,
+                                       HealthCheck.function_scoped_fixture])
+
+
+@st.composite
+def wide_ref_rounds(draw):
+    dtype = draw(st.sampled_from(sorted(_REF_RUNGS)))
+    lo, hi = draw(st.sampled_from(_REF_RUNGS[dtype]))
+    P = draw(st.integers(lo, hi))
+    K = draw(st.integers(1, 8))
+    w = draw(st.lists(st.one_of(st.integers(-50, 600), st.floats(-4.0, 4.0, width=32),
+                                st.sampled_from([0.37, 0.1, 1.7])), min_size=K, max_size=K))
+    split = draw(st.integers(0, K))  # rows before the acc_in continuation
+    off = draw(st.one_of(st.none(), st.integers(0, K - 1)))  # a row off 16-B alignment
+    seed = draw(st.integers(0, 2 ** 31 - 1))
+    return dtype, P, K, w, split, off, seed
+
+
+@WIDE
+@given(wide_ref_rounds())
+def test_generic_kernel_tiles_random(dev, case):
+    """fedagg_reduce_rows_ref at random sizes around every tile of the ladder,
+    vector or all-scalar path, one call or a running sum continued with
+    acc_in: bitwise the reference's CPU arithmetic (finite inputs)."""
+    from fedsim_amd import ops
+    from oracle.reference_loop import ReferenceSerialAggregator
+
+    dtype, P, K, w, split, off, seed = case
+    dt = getattr(torch, dtype)
+    g = torch.Generator().manual_seed(seed)
+    X = [(torch.randn(P, generator=g, dtype=torch.float32) * 0.5).to(dt) for _ in range(K)]
+    ref = ReferenceSerialAggregator()
+    for k in range(K):
+        ref.add("p", X[k], w[k])
+    want = ref.get_sum("p")
+    rows = [x.to(dev) for x in X]
+    if off is not None:
+        big = torch.empty(P + 1, dtype=dt, device=dev)
+        big[1:].copy_(X[off])
+        rows[off] = big[1:]
+    out = torch.empty(P, dtype=dt, device=dev)
+    if 0 < split < K:
+        head = torch.empty(P, dtype=dt, device=dev)
+        ops.reduce_rows_ref(rows[:split], w[:split], head)
+        ops.reduce_rows_ref(rows[split:], w[split:], out, acc_in=head)
+    else:
+        ops.reduce_rows_ref(rows, w, out)
+    got = out.cpu()
+    nan_g, nan_e = torch.isnan(got), torch.isnan(want)
+    assert torch.equal(nan_g, nan_e)
+    ib = torch.int64 if dt == torch.float64 else torch.int16
+    assert torch.equal(got[~nan_g].view(ib), want[~nan_e].view(ib))
+
+
+@WIDE
+@given(st.integers(1_500_000, 5_000_000), st.integers(1, 20), st.booleans(),
+       st.integers(0, 20), st.integers(0, 2 ** 31 - 1))
+def test_fp32_tile_rows_random(dev, P, K, finalize, split, seed):
+    """fedagg_reduce_rows_f32 on borrowed rows at random sizes around its tile
+    thresholds (P % 4 != 0 keeps the narrow kernels): bitwise the narrow
+    kernels (mapping forced), with the divide and an acc_in continuation."""
+    from fedsim_amd import ops
+
+    g = torch.Generator(device=dev).manual_seed(seed)
+    rows = [torch.empty(P, device=dev).normal_(0, 1, generator=g) for _ in range(K)]
+    wl = [float(v) for v in torch.randint(-5, 600, (K,), generator=torch.Generator().manual_seed(seed))]
+    wl[0] = 0.37
+    w32 = torch.tensor([ops.fl32(x) for x in wl], dtype=torch.float32, device=dev)
+    W = sum(wl) if finalize and sum(wl) != 0 else None
+    split = min(split, K)
+    outs = []
+    for flags in (0, 3 << 18):  # default mapping (tiles where they apply); FEDAGG_MAP VW=2
+        out = torch.empty(P, device=dev)
+        if 0 < split < K:
+            acc = torch.empty(P, device=dev)
+            ops.reduce_rows(rows[:split], w32[:split], acc, flags=flags)
+            ops.reduce_rows(rows[split:], w32[split:], out, acc_in=acc, W=W, flags=flags)
+        else:
+            ops.reduce_rows(rows, w32, out, W=W, flags=flags)
+        outs.append(out)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
