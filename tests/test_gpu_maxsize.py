@@ -123,3 +123,46 @@ def test_blocked_full_region_high_row_offsets(kcap):
         np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(want))
     del Xb
     torch.cuda.empty_cache()
+
+
+def test_max_P_tile_rows(data):
+    """The largest P that takes fedagg_reduce_rows_f32's wide-tile path
+    (2^30 - 4: P = 2^30 itself keeps the flat-load narrow kernel): the
+    sampled columns against the oracle, with the divide."""
+    from fedsim_amd import ops
+
+    P2 = P - 4
+    rows = [data["X"][k, :P2] for k in range(K)]
+    out = torch.empty(P2, dtype=torch.float32, device=data["dev"])
+    ops.reduce_rows(rows, data["w32"], out, W=sum(data["w"]))
+    keep = (data["idx"] < P2).cpu().numpy()
+    got = out[data["idx"][data["idx"] < P2]].cpu().numpy()
+    np.testing.assert_array_equal(bits(got), bits(data["want"][keep]))
+
+
+@pytest.mark.parametrize("dtype,P_big", [("bfloat16", (1 << 31) + 7), ("float64", (1 << 29) + 3)])
+def test_generic_kernel_rows_over_4_GiB(dtype, P_big):
+    """fedagg_reduce_rows_ref with rows of more than 4 GiB (64-bit element
+    offsets, the wide tile and the scalar tail): sampled columns, the last
+    ones included, bitwise the reference's CPU arithmetic on them."""
+    from fedsim_amd import ops
+    from oracle.reference_loop import ReferenceSerialAggregator
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(77)
+    rows = [torch.empty(P_big, dtype=dt, device=dev).uniform_(-1, 1, generator=g)
+            for _ in range(2)]
+    w = [3, 0.37]
+    out = torch.empty(P_big, dtype=dt, device=dev)
+    ops.reduce_rows_ref(rows, w, out)
+    rng = np.random.default_rng(8)
+    cols = np.unique(np.concatenate([rng.integers(0, P_big, 4096), np.arange(P_big - 70, P_big)]))
+    idx = torch.from_numpy(cols).to(dev)
+    ref_agg = ReferenceSerialAggregator()
+    for r, wk in zip(rows, w):
+        ref_agg.add("p", r[idx].cpu(), wk)
+    ib = torch.int64 if dt == torch.float64 else torch.int16
+    assert torch.equal(out[idx].cpu().view(ib), ref_agg.get_sum("p").view(ib))
+    del rows, out
+    torch.cuda.empty_cache()
