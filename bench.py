@@ -882,7 +882,7 @@ def _main(a, quiet):
     traffic, traffic_source = info.pop("_traffic", (None, None))
     result = {
         "metric": METRIC,
-        "value": round(value, 2),
+        "value": float(f"{value:.6g}"),  # 6 significant digits: tiny rehearsals stay > 0
         "unit": "GB/s",
         "n_gpus": rk.world,
         "steps": a.steps,
