@@ -17,6 +17,9 @@
 #                    build's md5, read by bench.py's roofline.traffic)
 #   feddf            tools/bench_feddf_teachers.py (replay vs vmap per batch)
 #   py=<script args> python3 tools/<script> with arguments (',' for spaces)
+#   pmcpy=<script args> FETCH_SIZE / WRITE_SIZE passes (+ the pmc_calib
+#                    calibration) over python3 tools/<script> (',' for spaces;
+#                    tools/pmc_rows_tiles.py reads them)
 #   sq=<script args> two SQ-counter passes (tools/sq_summary.py reads them)
 #                    over python3 tools/<script> (',' for spaces)
 #   hbm_peak         tools/hbm_peak read-stream ceiling
@@ -64,6 +67,13 @@ step() {
            --label "k_reduce_narrow<U=8, VW=2>" --width 2 \
            --calib-fetch "$OUT/calib_fetch" --calib-write "$OUT/calib_write" \
            --profile "profiles/$TAG/" --out "$OUT/pmc_traffic.json" ;;
+    pmcpy=*)
+      arg=${s#pmcpy=}
+      arg=${arg//,/ }
+      pmc FETCH_SIZE calib_fetch ./tools/pmc_calib \
+      && pmc WRITE_SIZE calib_write ./tools/pmc_calib \
+      && pmc FETCH_SIZE pmcpy_fetch python3 tools/$arg \
+      && pmc WRITE_SIZE pmcpy_write python3 tools/$arg ;;
     feddf)
       timeout -k 10 600 python -u tools/bench_feddf_teachers.py > "$OUT/feddf_teachers.jsonl" \
         2> "$OUT/feddf_teachers.err" ;;
