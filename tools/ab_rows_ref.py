@@ -75,7 +75,7 @@ def main():
     st = torch.cuda.current_stream()
     codes = {torch.bfloat16: _native.FEDAGG_DTYPE_BF16, torch.float16: _native.FEDAGG_DTYPE_F16,
              torch.float64: _native.FEDAGG_DTYPE_F64}
-    for name, mb in [(n, m) for m in a.row_mb.replace(":", ",").split(",") for n in a.dtypes.split(",")]:
+    for name, mb in [(n, m) for m in a.row_mb.replace(":", ",").split(",") for n in a.dtypes.replace(":", ",").split(",")]:
         dt = getattr(torch, name)
         esize = torch.empty((), dtype=dt).element_size()
         P = int(float(mb) * 1_000_000) // esize + a.odd
