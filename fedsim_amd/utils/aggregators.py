@@ -799,7 +799,7 @@ class _RefDeviceEntry(_TensorEntry):
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
         src = value.detach() if value.requires_grad else value
-        src = src.reshape(-1)
+        # rows are read flat by data pointer: no reshape view (~1 us per add)
         if self.borrow and src.is_contiguous():
             row = (src, src._version)  # handed over: read at the reduction
         else:

@@ -16,7 +16,6 @@ rounds (tests/golden/generic_keys.json, tools/gen_golden_generic.py).
 """
 import json
 import os
-import socket
 import tempfile
 
 import pytest
@@ -28,15 +27,13 @@ with open(os.path.join(GOLDEN_DIR, "generic_keys.json")) as _f:
     _GOLD = json.load(_f)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _file_store(d):
+    """A file rendezvous for the spawned gloo ranks: no TCP port to race for
+    (a port picked free and then bound by the store can be taken in between)."""
+    return "file://" + os.path.join(d, "pg_store")
 
 
-def _scenario_worker(rank, world, port, kind, mode, outdir):
+def _scenario_worker(rank, world, store, kind, mode, outdir):
     import torch.distributed as dist
 
     from fedsim_amd.sharding import (ClientShardedSerialAggregator, RemoteRow,
@@ -44,8 +41,7 @@ def _scenario_worker(rank, world, port, kind, mode, outdir):
     from oracle import generic_cases as G
     from shard_oracle import ChainOracleEntry, OracleEntry, oracle_step
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         out = {}
         for name, steps in G.scenarios().items():
@@ -73,7 +69,7 @@ def _scenario_worker(rank, world, port, kind, mode, outdir):
 @pytest.mark.parametrize("world", [2, 3])
 def test_generic_scenarios_every_rank(world, kind, mode):
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_scenario_worker, args=(world, _free_port(), kind, mode, d),
+        mp.start_processes(_scenario_worker, args=(world, _file_store(d), kind, mode, d),
                            nprocs=world, join=True, start_method="spawn")
         for r in range(world):
             with open(os.path.join(d, f"rank{r}.json")) as f:
@@ -82,7 +78,7 @@ def test_generic_scenarios_every_rank(world, kind, mode):
                 assert got[name] == want, (kind, mode, world, r, name)
 
 
-def _rounds_worker(rank, world, port, run_ids, mode, outdir):
+def _rounds_worker(rank, world, store, run_ids, mode, outdir):
     import random
     from functools import partial
 
@@ -95,8 +91,7 @@ def _rounds_worker(rank, world, port, run_ids, mode, outdir):
     from oracle import synthetic_fl as S
     from shard_oracle import ChainOracleEntry
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         runs = {r["id"]: r for r in _GOLD["dtype_runs"]}
         out = {}
@@ -140,7 +135,7 @@ def test_generic_client_sharded_rounds(world, mode):
     runs = [r for r in _GOLD["dtype_runs"] if r["algorithm"] != "AdaBest"]
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_rounds_worker,
-                           args=(world, _free_port(), [r["id"] for r in runs], mode, d),
+                           args=(world, _file_store(d), [r["id"] for r in runs], mode, d),
                            nprocs=world, join=True, start_method="spawn")
         for r in range(world):
             with open(os.path.join(d, f"rounds{r}.json")) as f:

@@ -3,7 +3,8 @@ reducer, on a one-rank RCCL ("nccl") process group (the 8-GPU run belongs to the
 driver).  Bit-exact vs the oracle for param / chain; the all-reduce path must
 still be exact at one rank (nothing is reordered)."""
 import os
-import socket
+import shutil
+import tempfile
 
 import numpy as np
 import pytest
@@ -16,12 +17,11 @@ from oracle import vectors as V
 pytestmark = pytest.mark.gpu
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _file_store(d):
+    """A file rendezvous for the spawned gloo ranks: no TCP port to race
+    for (a port picked free and then bound by the store can be taken in
+    between: EADDRINUSE on a shared box, r05ae)."""
+    return "file://" + os.path.join(d, "pg_store")
 
 
 @pytest.fixture(scope="module")
@@ -31,12 +31,12 @@ def pg():
     if dist.is_initialized():
         yield dist
         return
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(_port())
-    dist.init_process_group("nccl", rank=0, world_size=1,
+    d = tempfile.mkdtemp()
+    dist.init_process_group("nccl", init_method=_file_store(d), rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     yield dist
     dist.destroy_process_group()
+    shutil.rmtree(d, ignore_errors=True)
 
 
 @pytest.mark.parametrize("mode", ["param", "chain", "allreduce"])
@@ -133,7 +133,7 @@ def test_sharded_round_loop_one_rank_rccl(run, device, pg, round_arrays):
     _check_run(run, alg.get_server_storage(), scores, round_arrays, device)
 
 
-def _gloo_gpu_worker(rank, world, port, ids, outdir):
+def _gloo_gpu_worker(rank, world, store, ids, outdir):
     """One rank of a gloo group whose ranks share cuda:0 (HIP entries; the
     shards are exchanged through host memory)."""
     import json
@@ -143,9 +143,8 @@ def _gloo_gpu_worker(rank, world, port, ids, outdir):
 
     from fedsim_amd.sharding import ShardedSerialAggregator
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         runs = {r["id"]: r for r in _golden_runs()}
         for rid in ids:
@@ -178,7 +177,7 @@ def test_sharded_round_loop_two_ranks_on_one_gpu(round_arrays):
 
     ids = [r["id"] for r in SYN_RUNS]
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_gpu_worker, args=(2, _port(), ids, d), nprocs=2, join=True,
+        mp.start_processes(_gloo_gpu_worker, args=(2, _file_store(d), ids, d), nprocs=2, join=True,
                            start_method="spawn")
         for run in SYN_RUNS:
             for r in range(2):
@@ -347,7 +346,7 @@ def test_client_sharded_round_loop_one_rank_rccl(run, device, mode, pg, round_ar
     _check_run(run, alg.get_server_storage(), scores, round_arrays, f"{device} {mode}")
 
 
-def _gloo_gpu_client_worker(rank, world, port, ids, mode, outdir):
+def _gloo_gpu_client_worker(rank, world, store, ids, mode, outdir):
     """One rank of a gloo group sharing cuda:0: trains its block of clients,
     HIP entries, the chain / all-reduce through host memory."""
     import json
@@ -357,9 +356,8 @@ def _gloo_gpu_client_worker(rank, world, port, ids, mode, outdir):
 
     from fedsim_amd.sharding import ClientShardedSerialAggregator
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         runs = {r["id"]: r for r in _golden_runs()}
         for rid in ids:
@@ -392,7 +390,7 @@ def test_client_sharded_round_loop_two_ranks_on_one_gpu(mode, round_arrays):
 
     ids = [r["id"] for r in CS_RUNS]
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_gpu_client_worker, args=(2, _port(), ids, mode, d), nprocs=2,
+        mp.start_processes(_gloo_gpu_client_worker, args=(2, _file_store(d), ids, mode, d), nprocs=2,
                            join=True, start_method="spawn")
         for run in CS_RUNS:
             for r in range(2):
@@ -415,7 +413,7 @@ def test_client_sharded_round_loop_two_ranks_on_one_gpu(mode, round_arrays):
                     assert scores == run["scores"]
 
 
-def _gloo_gpu_feddf_worker(rank, world, port, mode, outdir):
+def _gloo_gpu_feddf_worker(rank, world, store, mode, outdir):
     """One rank of a gloo group sharing cuda:0: a FedDF round loop on the
     reference's CNNs whose teachers are replayed per rank on the HIP kernels
     and combined by the client-sharded aggregator."""
@@ -432,9 +430,8 @@ def _gloo_gpu_feddf_worker(rank, world, port, mode, outdir):
     from fedsim_amd.sharding import ClientShardedSerialAggregator
     from oracle import synthetic_fl as S
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         with open(os.path.join(GOLDEN_DIR, "feddf_cnn.json")) as f:
             G = json.load(f)
@@ -497,7 +494,7 @@ def test_client_sharded_feddf_two_ranks_on_one_gpu(mode):
     with np.load(os.path.join(GOLDEN_DIR, "feddf_cnn.npz"), allow_pickle=False) as z:
         golden = {k: z[k] for k in z.files}
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_gpu_feddf_worker, args=(2, _port(), mode, d), nprocs=2,
+        mp.start_processes(_gloo_gpu_feddf_worker, args=(2, _file_store(d), mode, d), nprocs=2,
                            join=True, start_method="spawn")
         for run in G["runs"]:
             rid = run["id"]
@@ -621,7 +618,7 @@ def test_sharded_generic_key_one_rank(dtype, pg):
     assert encode(agg.pop("p")) == encode(ref.pop("p"))
 
 
-def _gloo_dtype_worker(rank, world, port, outdir):
+def _gloo_dtype_worker(rank, world, store, outdir):
     import json
     from functools import partial
 
@@ -629,9 +626,8 @@ def _gloo_dtype_worker(rank, world, port, outdir):
 
     from fedsim_amd.sharding import ShardedSerialAggregator
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         out = {}
         for run in _dtype_runs():
@@ -654,7 +650,7 @@ def test_sharded_dtype_rounds_two_ranks_on_one_gpu():
     import torch.multiprocessing as mp
 
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_dtype_worker, args=(2, _port(), d), nprocs=2, join=True,
+        mp.start_processes(_gloo_dtype_worker, args=(2, _file_store(d), d), nprocs=2, join=True,
                            start_method="spawn")
         for r in range(2):
             with open(os.path.join(d, f"dtype_rank{r}.json")) as f:

@@ -11,7 +11,6 @@ FedAvg / AdaBest / FedNova / FedDyn through CentralFLAlgorithm, every rank
 holding the full model after each round, bitwise against the goldens.
 """
 import os
-import socket
 import tempfile
 
 import numpy as np
@@ -24,12 +23,10 @@ from oracle import ref
 from oracle import vectors as V
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _file_store(d):
+    """A file rendezvous for the spawned gloo ranks: no TCP port to race for
+    (a port picked free and then bound by the store can be taken in between)."""
+    return "file://" + os.path.join(d, "pg_store")
 
 
 def oracle_reduce(X, w32, out, acc_in, W, flags):
@@ -41,13 +38,12 @@ def oracle_reduce(X, w32, out, acc_in, W, flags):
     return out
 
 
-def _worker(rank, world, port, K, P, mode, outdir):
+def _worker(rank, world, store, K, P, mode, outdir):
     import torch.distributed as dist
 
     from fedsim_amd import sharding
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         X = torch.from_numpy(V.client_rows("normal", K, P, 21))
         w = V.client_weights("fedavg", K, 21)
@@ -88,7 +84,7 @@ def _worker(rank, world, port, K, P, mode, outdir):
 def test_sharded_protocols(mode, world):
     K, P = 23, 4099
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), K, P, mode, d), nprocs=world,
+        mp.start_processes(_worker, args=(world, _file_store(d), K, P, mode, d), nprocs=world,
                            join=True, start_method="spawn")
         X = V.client_rows("normal", K, P, 21)
         w = V.client_weights("fedavg", K, 21)
@@ -127,7 +123,7 @@ def test_shard_range_covers_and_aligns():
 # ---------------------------------------------------------------------------
 # ShardedSerialAggregator through the round driver
 # ---------------------------------------------------------------------------
-def _rounds_worker(rank, world, port, run_ids, outdir):
+def _rounds_worker(rank, world, store, run_ids, outdir):
     import json
     import random
     from functools import partial
@@ -141,8 +137,7 @@ def _rounds_worker(rank, world, port, run_ids, outdir):
     import shard_oracle
     from shard_oracle import OracleEntry
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         with open(os.path.join(GOLDEN_DIR, "rounds.json")) as f:
             runs = {r["id"]: r for r in json.load(f)["runs"]}
@@ -194,7 +189,7 @@ def test_sharded_aggregator_round_loop_bitwise(world):
     with np.load(os.path.join(GOLDEN_DIR, "rounds.npz"), allow_pickle=False) as z:
         arrays = {k: z[k] for k in z.files}
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rounds_worker, args=(world, _free_port(), ids, d), nprocs=world,
+        mp.start_processes(_rounds_worker, args=(world, _file_store(d), ids, d), nprocs=world,
                            join=True, start_method="spawn")
         for run in runs:
             for r in range(world):
@@ -272,7 +267,7 @@ def test_client_sharded_add_after_get_is_refused():
     assert torch.equal(agg.pop("local_params"), got)
 
 
-def _api_worker(rank, world, port, outdir):
+def _api_worker(rank, world, store, outdir):
     """Every SerialAggregator call on a parameter-sharded key, including
     shards that are empty (P < 64 * world), against the one-process oracle."""
     import json
@@ -283,8 +278,7 @@ def _api_worker(rank, world, port, outdir):
     from fedsim_amd.sharding import ShardedSerialAggregator
     from shard_oracle import OracleEntry
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     out = {}
     try:
         for P in (1, 63, 65, 130, 4099):
@@ -323,7 +317,7 @@ def test_sharded_aggregator_api_every_rank():
 
     world = 3
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_api_worker, args=(world, _free_port(), d), nprocs=world, join=True,
+        mp.start_processes(_api_worker, args=(world, _file_store(d), d), nprocs=world, join=True,
                            start_method="spawn")
         got = [json.load(open(os.path.join(d, f"api{r}.json"))) for r in range(world)]
     for P in (1, 63, 65, 130, 4099):
@@ -357,7 +351,7 @@ def test_sharded_aggregator_api_every_rank():
 # ---------------------------------------------------------------------------
 # ClientShardedSerialAggregator through the round driver
 # ---------------------------------------------------------------------------
-def _client_rounds_worker(rank, world, port, run_ids, mode, outdir):
+def _client_rounds_worker(rank, world, store, run_ids, mode, outdir):
     import json
     import random
     from functools import partial
@@ -371,8 +365,7 @@ def _client_rounds_worker(rank, world, port, run_ids, mode, outdir):
     import shard_oracle
     from shard_oracle import ChainOracleEntry, oracle_step
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         with open(os.path.join(GOLDEN_DIR, "rounds.json")) as f:
             runs = {r["id"]: r for r in json.load(f)["runs"]}
@@ -439,7 +432,7 @@ def test_client_sharded_round_loop(world, mode):
         arrays = {k: z[k] for k in z.files}
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_client_rounds_worker,
-                           args=(world, _free_port(), [r["id"] for r in runs], mode, d),
+                           args=(world, _file_store(d), [r["id"] for r in runs], mode, d),
                            nprocs=world, join=True, start_method="spawn")
         for run in runs:
             trained = []
@@ -472,7 +465,7 @@ def test_client_sharded_round_loop(world, mode):
             assert sum(per_round) == 5 * 5 and all(n < 25 for n in per_round), per_round
 
 
-def _client_extras_worker(rank, world, port, outdir):
+def _client_extras_worker(rank, world, store, outdir):
     """Stateful clients, a diverged client and FedDF under client sharding."""
     import json
     import random
@@ -485,8 +478,7 @@ def _client_extras_worker(rank, world, port, outdir):
     from oracle import synthetic_fl as S
     from shard_oracle import ChainOracleEntry, oracle_step
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     factory = partial(ClientShardedSerialAggregator, entry_factory=ChainOracleEntry,
                       step_impl=oracle_step)
     res = {}
@@ -666,7 +658,7 @@ def test_client_sharded_state_divergence_and_refusal():
 
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_client_extras_worker, args=(world, _free_port(), d), nprocs=world,
+        mp.start_processes(_client_extras_worker, args=(world, _file_store(d), d), nprocs=world,
                            join=True, start_method="spawn")
         res = [json.load(open(os.path.join(d, f"extras_rank{r}.json"))) for r in range(world)]
     assert res[1]["failure"] == "own: client failure on rank 1"
@@ -696,7 +688,7 @@ def test_client_sharded_state_divergence_and_refusal():
 # ---------------------------------------------------------------------------
 # FedDF under client-sharded rounds: the reference's own CNN rounds
 # ---------------------------------------------------------------------------
-def _feddf_worker(rank, world, port, mode, outdir):
+def _feddf_worker(rank, world, store, mode, outdir):
     import json
     import random
     from functools import partial
@@ -711,8 +703,7 @@ def _feddf_worker(rank, world, port, mode, outdir):
     from oracle import synthetic_fl as S
     from shard_oracle import ChainOracleEntry, oracle_step
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=store, rank=rank, world_size=world)
     try:
         with open(os.path.join(GOLDEN_DIR, "feddf_cnn.json")) as f:
             G = json.load(f)
@@ -780,7 +771,7 @@ def test_client_sharded_feddf_matches_reference(world, mode):
     with np.load(os.path.join(GOLDEN_DIR, "feddf_cnn.npz"), allow_pickle=False) as z:
         golden = {k: z[k] for k in z.files}
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_feddf_worker, args=(world, _free_port(), mode, d), nprocs=world,
+        mp.start_processes(_feddf_worker, args=(world, _file_store(d), mode, d), nprocs=world,
                            join=True, start_method="spawn")
         for run in G["runs"]:
             rid = run["id"]
