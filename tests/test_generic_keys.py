@@ -236,3 +236,37 @@ def test_reference_kernel_tile_rungs(dtype, rung, aligned):
     tail = torch.empty(P, dtype=dt, device=dev)
     ops.reduce_rows_ref(rows[6:], w[6:], tail, acc_in=head)
     assert torch.equal(tail.view(ib), out.view(ib))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float64"])
+def test_generic_key_borrow_and_snapshot_semantics(dtype):
+    """A handed-over (borrowed) HBM row of a generic key changed in place
+    after add makes the reduction raise, every time it is asked for; a
+    snapshotting aggregator keeps the value as it was at add (the
+    reference's clone, training/utils.py:34)."""
+    from fedsim_amd.utils import SerialAggregator
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(4)
+    X = [(torch.randn(5000, generator=g) * 0.3).to(dt) for _ in range(3)]
+    ref = ReferenceSerialAggregator()
+    for x in X:
+        ref.add("p", x, 7)
+
+    agg = SerialAggregator(borrow=True)
+    vals = [x.to(dev) for x in X]
+    for v in vals:
+        agg.add("p", v, 7)
+    vals[1].mul_(2)
+    for _ in range(2):
+        with pytest.raises(RuntimeError, match="modified in place"):
+            agg.get_sum("p")
+
+    snap = SerialAggregator(borrow=False)
+    vals = [x.to(dev) for x in X]
+    for v in vals:
+        snap.add("p", v, 7)
+    vals[1].mul_(2)
+    assert G.encode(snap.pop("p")) == G.encode(ref.pop("p"))
