@@ -86,3 +86,20 @@ def test_tile_rows_no_rows_is_the_running_sum():
     assert rc == 0
     want = acc.cpu().numpy() / np.float32(3.0)  # IEEE division per element
     assert np.array_equal(out.cpu().numpy().view(np.int32), want.view(np.int32))
+
+
+@pytest.mark.parametrize("P", [4_200_000, 3_000_004], ids=["4x8", "8x4"])
+def test_tile_rows_in_place_running_sum(P):
+    """The aggregator's drains continue the running sum in place (out is
+    acc_in, _DeviceEntry._flush_borrowed): the same bits as one call."""
+    K = 19
+    rows = _rows(P, K, seed=11)
+    wl = [float(3 + 5 * k) for k in range(K)]
+    w32 = torch.tensor(wl, dtype=torch.float32, device="cuda")
+    whole = torch.empty(P, device="cuda")
+    ops.reduce_rows(rows, w32, whole, W=sum(wl))
+    acc = torch.empty(P, device="cuda")
+    ops.reduce_rows(rows[:5], w32[:5], acc)
+    ops.reduce_rows(rows[5:12], w32[5:12], acc, acc_in=acc)
+    ops.reduce_rows(rows[12:], w32[12:], acc, acc_in=acc, W=sum(wl))
+    assert torch.equal(acc.view(torch.int32), whole.view(torch.int32))
