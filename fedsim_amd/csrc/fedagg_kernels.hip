@@ -3922,6 +3922,8 @@ int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out, void
 int fedagg_reduce_rows_ref(int dtype, const void* const* rows, const void* w, int64_t B,
                            int64_t P, const void* acc_in, void* out, int flags, void* stream) {
   const bool init = (flags & FEDAGG_INIT) != 0;
+  if (dtype != FEDAGG_DTYPE_BF16 && dtype != FEDAGG_DTYPE_F16 && dtype != FEDAGG_DTYPE_F64)
+    return FEDAGG_EINVAL;
   if (P < 0 || B < 0 || (init && B == 0)) return FEDAGG_EINVAL;
   if (flags & ~(FEDAGG_INIT | FEDAGG_SCALAR)) return FEDAGG_EINVAL;
   if (P == 0) return 0;

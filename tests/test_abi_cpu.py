@@ -339,3 +339,32 @@ def test_build_is_reproducible():
     assert rec["identical"] and rec["builds"][0]["md5"] == rec["builds"][1]["md5"]
     assert rec["builds"][0]["dir"] != rec["builds"][1]["dir"]
     assert rec["flags"] == G.HIP_FLAGS
+
+
+def test_reduce_rows_ref_rejects_bad_arguments():
+    """fedagg_reduce_rows_ref validates before any HIP call (none is made
+    here: no GPU): an unknown dtype, negative sizes, INIT without rows, flags
+    it does not take, missing pointers -> FEDAGG_EINVAL; P = 0 is a no-op."""
+    from fedsim_amd import _native
+
+    lib = _native.load()
+    f = lib.fedagg_reduce_rows_ref
+    E, INIT, BF16, F64 = (_native.FEDAGG_EINVAL, _native.FEDAGG_INIT,
+                          _native.FEDAGG_DTYPE_BF16, _native.FEDAGG_DTYPE_F64)
+    p = 4096  # a pointer value: never dereferenced on these paths
+    bad = [
+        (0, p, p, 1, 8, None, p, INIT),            # dtype 0
+        (4, p, p, 1, 8, None, p, INIT),            # dtype past the last code
+        (BF16, p, p, 1, -1, None, p, INIT),        # P < 0
+        (BF16, p, p, -1, 8, p, p, 0),              # B < 0
+        (F64, p, p, 0, 8, None, p, INIT),          # INIT with no rows
+        (BF16, p, p, 1, 8, None, p, INIT | _native.FEDAGG_FINALIZE),  # flag it does not take
+        (BF16, p, p, 1, 8, None, None, INIT),      # no out
+        (BF16, p, p, 1, 8, None, p, 0),            # continuing without acc_in
+        (BF16, None, p, 1, 8, None, p, INIT),      # rows missing
+        (F64, p, None, 1, 8, None, p, INIT),       # weights missing
+        (0, p, p, 1, 0, None, p, INIT),            # unknown dtype even at P = 0
+    ]
+    for args in bad:
+        assert f(*args, None) == E, args
+    assert f(BF16, p, p, 1, 0, None, p, INIT, None) == 0  # P = 0: nothing to do
