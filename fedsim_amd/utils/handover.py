@@ -40,6 +40,8 @@ from typing import Optional
 
 import torch
 
+from .slab_rows import SlabRow
+
 __all__ = ["hand_over", "handover_round", "take_token", "unaliased"]
 
 
@@ -102,8 +104,6 @@ def _storage_key(t):
 def unaliased(t) -> bool:
     """No other tensor (view, base, alias) shares ``t``'s storage: one
     TensorImpl on it plus the temporary storage object made here."""
-    from .slab_rows import SlabRow
-
     if not isinstance(t, torch.Tensor) or t._base is not None:
         return False
     if isinstance(t, SlabRow):
