@@ -6,7 +6,9 @@ narrow kernels with the mapping forced and against numpy float32 on sampled
 columns.  Random P (log-uniform, 1 .. 9 M), K, weights (integers, tie-prone
 decimals, negatives, zero), values (normal at several scales, with +-0,
 +-inf, NaN, subnormals and huge values mixed in), a row off 16-B alignment,
-and a running sum continued through acc_in.  NaN positions are compared as
+and a running sum continued through acc_in; and whole fp32 drop-in
+sessions (agg: HBM / host rows, borrowed or not, ring drains, a get
+mid-stream) against the reference's CPU SerialAggregator.  NaN positions are compared as
 NaN (their bits are not pinned by the reference).  Prints one JSON line per
 100 cases and a summary; exit 1 on the first mismatch, with the case.
 
@@ -121,6 +123,36 @@ def f32_case(rng, dev):
     return ok, dict(kind="f32", P=P, K=K, w=wl, special=special, W=W, split=split)
 
 
+def agg_case(rng, dev):
+    """A whole drop-in session on fp32 client vectors: HBM (borrowed or
+    snapshotted) or host rows, ring drains at a random max_rows, a get
+    mid-stream, then pop -- against the reference's CPU SerialAggregator."""
+    from fedsim_amd.utils import SerialAggregator
+
+    P = int(math.exp(rng.uniform(0, math.log(4_000_000))))
+    K = rng.randint(1, 24)
+    special = rng.random() < 0.2
+    X = values(rng, P, K, torch.float32, special)
+    w = [x if rng.random() < 0.7 else float(x) for x in weights(rng, K)]
+    borrow = rng.random() < 0.5
+    agg = SerialAggregator(max_rows=rng.randint(1, 30), borrow=borrow)
+    ref = ReferenceSerialAggregator()
+    where = [rng.choice(["hbm", "hbm", "host"]) for _ in range(K)]
+    mid = rng.randrange(K)
+    ok = True
+    for k in range(K):
+        v = X[k].to(dev) if where[k] == "hbm" else X[k].clone()
+        agg.add("p", v, w[k])
+        ref.add("p", X[k], w[k])
+        if k == mid:
+            g, e = agg.get("p"), ref.get("p")
+            ok = ok and same(g.cpu() if isinstance(g, torch.Tensor) else g, e, torch.int32)
+    got, want = agg.pop("p"), ref.pop("p")
+    ok = ok and same(got.cpu(), want, torch.int32)
+    return ok, dict(kind="agg", P=P, K=K, w=w, special=special, borrow=borrow, where=where,
+                    mid=mid)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=300)
@@ -128,10 +160,10 @@ def main():
     a = ap.parse_args()
     rng = random.Random(a.seed)
     dev = torch.device("cuda:0")
-    t0, n, counts = time.time(), 0, {"generic": 0, "f32": 0}
+    t0, n, counts = time.time(), 0, {"generic": 0, "f32": 0, "agg": 0}
     while time.time() - t0 < a.seconds:
-        kind = rng.choice(["generic", "f32"])
-        ok, case = (generic_case if kind == "generic" else f32_case)(rng, dev)
+        kind = rng.choice(["generic", "f32", "agg"])
+        ok, case = {"generic": generic_case, "f32": f32_case, "agg": agg_case}[kind](rng, dev)
         n += 1
         counts[kind] += 1
         if not ok:
