@@ -12,7 +12,7 @@ mid-stream) against the reference's CPU SerialAggregator.  NaN positions are com
 NaN (their bits are not pinned by the reference).  Prints one JSON line per
 100 cases and a summary; exit 1 on the first mismatch, with the case.
 
-python tools/fuzz_tiles.py [--seconds 300] [--seed 1]
+python tools/fuzz_tiles.py [--seconds 300] [--seed 1] [--min-p 1]
 """
 import argparse
 import json
@@ -31,6 +31,12 @@ from oracle.reference_loop import ReferenceSerialAggregator  # noqa: E402
 
 MAP_VW2 = 3 << 18
 SPECIALS = [0.0, -0.0, math.inf, -math.inf, math.nan, 1e-42, 3e-39, 6.5e4, 3e38]
+MIN_P = 1
+
+
+def draw_p(rng, hi):
+    lo = min(MIN_P, hi)
+    return int(math.exp(rng.uniform(math.log(lo), math.log(hi))))
 
 
 def values(rng, P, K, dt, special):
@@ -59,7 +65,7 @@ def same(got, want, ib):
 
 def generic_case(rng, dev):
     dt = rng.choice([torch.bfloat16, torch.float16, torch.float64])
-    P = int(math.exp(rng.uniform(0, math.log(9_000_000 if dt != torch.float64 else 3_600_000))))
+    P = draw_p(rng, 9_000_000 if dt != torch.float64 else 3_600_000)
     K = rng.randint(1, 12)
     special = rng.random() < 0.3
     X = values(rng, P, K, dt, special)
@@ -89,7 +95,7 @@ def generic_case(rng, dev):
 
 
 def f32_case(rng, dev):
-    P = int(math.exp(rng.uniform(0, math.log(9_000_000))))
+    P = draw_p(rng, 9_000_000)
     K = rng.randint(1, 16)
     special = rng.random() < 0.2
     X = values(rng, P, K, torch.float32, special)
@@ -129,7 +135,7 @@ def agg_case(rng, dev):
     mid-stream, then pop -- against the reference's CPU SerialAggregator."""
     from fedsim_amd.utils import SerialAggregator
 
-    P = int(math.exp(rng.uniform(0, math.log(4_000_000))))
+    P = draw_p(rng, 4_000_000)
     K = rng.randint(1, 24)
     special = rng.random() < 0.2
     X = values(rng, P, K, torch.float32, special)
@@ -157,8 +163,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=300)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--min-p", type=int, default=1, help="smallest P drawn (the tiles: 1000000)")
     a = ap.parse_args()
     rng = random.Random(a.seed)
+    global MIN_P
+    MIN_P = a.min_p
     dev = torch.device("cuda:0")
     t0, n, counts = time.time(), 0, {"generic": 0, "f32": 0, "agg": 0}
     while time.time() - t0 < a.seconds:
