@@ -3,7 +3,8 @@
 mismatch count, first indices and values (tests/test_generic_keys.py
 test_reference_kernel_tile_rungs is the pass / fail form).
 
-python tools/debug_rows_ref.py
+python tests/debug_rows_ref.py  (a GPU script, not collected by pytest; the
+oracle is its checker)
 """
 import json
 import os
@@ -12,7 +13,6 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 from fedsim_amd import ops  # noqa: E402
 
 

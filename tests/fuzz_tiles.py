@@ -12,7 +12,10 @@ mid-stream) against the reference's CPU SerialAggregator.  NaN positions are com
 NaN (their bits are not pinned by the reference).  Prints one JSON line per
 100 cases and a summary; exit 1 on the first mismatch, with the case.
 
-python tools/fuzz_tiles.py [--seconds 300] [--seed 1] [--min-p 1]
+python tests/fuzz_tiles.py [--seconds 300] [--seed 1] [--min-p 1]
+
+(a GPU script kept with the tests, not collected by pytest: the oracle is its
+checker)
 """
 import argparse
 import json

@@ -3,10 +3,9 @@ vectors of a bf16 / fp16 / fp64 model, ``add`` x K then ``pop``, through
 
   kernel  fedsim_amd's SerialAggregator: fedagg_reduce_rows_ref, borrowed
           (handed-over) or snapshotted rows
-  torch   the reference's own expression on the same HIP tensors
-          (oracle/reference_loop.ReferenceSerialAggregator: value * weight,
-          sum + new_v, two torch launches and three passes per client) --
-          what the keys ran as before the kernel
+  torch   the reference's own expression on the same HIP tensors (value *
+          weight, sum + new_v: two torch launches and three passes per
+          client) -- what the keys ran as before the kernel
 
 timed with HIP events; client bytes reduced per second.  The two sums are
 compared bit for bit (the quotient differs by design: torch's HIP division
@@ -23,7 +22,23 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedsim_amd.utils import SerialAggregator  # noqa: E402
-from oracle.reference_loop import ReferenceSerialAggregator  # noqa: E402
+
+
+class TorchExpression(object):
+    """The timed baseline leg: the reference's add / get_sum expression
+    (aggregators.py:17-40) written out on the same HIP tensors -- value *
+    weight, then sum + new_v, two torch launches and three passes per
+    client -- what the keys ran as before the kernel."""
+
+    def __init__(self):
+        self.sum_v, self.cur_w = 0, 0
+
+    def add(self, key, value, weight):
+        new_v = value * weight
+        self.sum_v, self.cur_w = self.sum_v + new_v, self.cur_w + weight
+
+    def get_sum(self, key):
+        return self.sum_v
 
 
 def main():
@@ -46,7 +61,7 @@ def main():
         for mode in ("kernel_borrow", "kernel_snapshot", "torch"):
             best = None
             for _ in range(a.reps):
-                agg = (ReferenceSerialAggregator() if mode == "torch" else
+                agg = (TorchExpression() if mode == "torch" else
                        SerialAggregator(borrow=mode == "kernel_borrow"))
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

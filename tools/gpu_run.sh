@@ -20,6 +20,8 @@
 #   pmcpy=<script args> FETCH_SIZE / WRITE_SIZE passes (+ the pmc_calib
 #                    calibration) over python3 tools/<script> (',' for spaces;
 #                    tools/pmc_rows_tiles.py reads them)
+#   tpy=<script args> python3 tests/<script> (the GPU checker scripts kept with
+#                    the tests: fuzz_tiles.py, debug_rows_ref.py)
 #   sq=<script args> two SQ-counter passes (tools/sq_summary.py reads them)
 #                    over python3 tools/<script> (',' for spaces)
 #   hbm_peak         tools/hbm_peak read-stream ceiling
@@ -82,6 +84,11 @@ step() {
       arg=${arg//,/ }
       timeout -k 10 ${PY_TIMEOUT:-600} python3 -u tools/$arg > "$OUT/py_$(echo "${arg%% *}" | tr '/.' '__').out" \
         2> "$OUT/py_$(echo "${arg%% *}" | tr '/.' '__').err" ;;
+    tpy=*)
+      arg=${s#tpy=}
+      arg=${arg//,/ }
+      timeout -k 10 ${PY_TIMEOUT:-600} python3 -u tests/$arg > "$OUT/tpy_$(echo "${arg%% *}" | tr '/.' '__').out" \
+        2> "$OUT/tpy_$(echo "${arg%% *}" | tr '/.' '__').err" ;;
     sq=*)
       arg=${s#sq=}
       arg=${arg//,/ }
