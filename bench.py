@@ -85,10 +85,15 @@ def parse(argv=None):
     ap.add_argument("--no-epilogue", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-side-legs", action="store_true",
+                    help="skip the N=1 side legs after the headline (h2d_inclusive: the "
+                         "host-to-host round; configs: BASELINE configs 2 / 3)")
     ap.add_argument("--no-selftest", action="store_true",
                     help="skip the multi-GPU self-test that precedes the timed region")
     ap.add_argument("--selftest-fault-rank", type=int, default=None,
                     help="TEST ONLY: flip one result bit on this rank in the self-test")
+    ap.add_argument("--selftest-fault-devices", action="store_true",
+                    help="TEST ONLY: fail rank 0's devices_* check in the self-test")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--master-port", type=int, default=0,
                     help="rendezvous port of the self-spawned ranks (0: pick a free one)")
@@ -515,7 +520,7 @@ def _rehearsal_entry():
     return Entry
 
 
-def multi_gpu_selftest(rk, fault_rank=None):
+def multi_gpu_selftest(rk, fault_rank=None, fault_devices=False):
     """One small round through every multi-GPU path over the job's real
     process group (RCCL on the GPUs; gloo in the rehearsal), each checked
     against the C oracle (oracle/ref.py) on every column: SURVEY §8e's
@@ -532,6 +537,10 @@ def multi_gpu_selftest(rk, fault_rank=None):
                           (vs oracle/reference_loop)                 bitwise
       param_sharded_step  sharding.param_sharded_step on this rank's column
                           shard (blocked slab, fused step)           bitwise
+      devices_*           rank 0, when it sees > 1 GPU: the one-process
+                          ShardedSerialAggregator(devices=[...]) on host /
+                          pinned / HBM vectors, get / pop / momentum
+                          pop_step with host and HBM clouds          bitwise
 
     Every rank checks its own result; the verdicts are combined with a MIN
     all-reduce, so every rank agrees.  Returns the dict that goes into the
@@ -627,6 +636,16 @@ def multi_gpu_selftest(rk, fault_rank=None):
         got = got.copy()
         got.view(np.uint32)[:1] ^= 1
     record("param_sharded_step", got, cloud_ref[lo:hi])
+    # (4) the single-process multi-GPU mode (every local GPU, one process), on
+    # rank 0 only, fenced by barriers so no collective of the others overlaps
+    rk.barrier()
+    devices = None
+    if me == 0:
+        devices = devices_selftest(rk, X, w, W, avg_ref, cloud0, record)
+        if fault_devices:  # TEST ONLY: a failing devices_* check must fail every rank
+            checks["devices_get_pageable"] = dict(bitwise=True, columns=P, mismatched=1,
+                                                  ok=False, injected=True)
+    rk.barrier()
     ok = all(c["ok"] for c in checks.values())
     if rk.dist is not None:  # every rank's verdict, agreed by all
         t = torch.tensor([1 if ok else 0], dtype=torch.int32,
@@ -639,7 +658,64 @@ def multi_gpu_selftest(rk, fault_rank=None):
                 world=world, backend=rk.dist.get_backend() if rk.dist else None,
                 K=K, P=P, seconds=round(time.perf_counter() - t0, 3),
                 checker="oracle/ref.py (C restatement, pinned to the reference's goldens)",
+                devices=(devices if devices is not None else
+                         "rank 0: ShardedSerialAggregator(devices=%d local GPUs)"
+                         % rk.torch.cuda.device_count()) if me == 0 else None,
                 checks=checks)
+
+
+def devices_selftest(rk, X, w, W, avg_ref, cloud0, record):
+    """ShardedSerialAggregator(devices=[every local GPU]) -- the one-process
+    multi-GPU mode FedSim's own simulator would use (one aggregator per round
+    in one process, centralized_fl_algorithm.py:417-429) -- checked on rank 0
+    against the C oracle, bitwise: get / pop with pageable, pinned and HBM
+    client vectors, and a momentum SGD pop_step with the cloud on the host and
+    in HBM.  Records ``devices_*`` checks; returns the skip reason (or None)."""
+    import torch
+
+    from fedsim_amd import ops
+    from fedsim_amd.sharding import ShardedSerialAggregator
+
+    if rk.rehearsal:
+        return "skipped: no HIP device (CPU rehearsal)"
+    n = torch.cuda.device_count()
+    if n < 2:
+        return "skipped: 1 device"
+    devs = list(range(n))
+    K, P = X.shape
+    src = {"pageable": lambda k: torch.from_numpy(X[k].copy()),
+           "pinned": lambda k: torch.from_numpy(X[k].copy()).pin_memory(),
+           "hbm": lambda k: torch.from_numpy(X[k].copy()).to(rk.dev)}
+    for name, make in src.items():
+        agg = ShardedSerialAggregator(devices=devs)
+        for k in range(K):
+            agg.add("p", make(k), w[k])
+        got = agg.get("p")
+        record("devices_get_" + name, got.cpu().numpy(), avg_ref)
+        record("devices_pop_" + name, agg.pop("p").cpu().numpy(), avg_ref)
+    # momentum SGD (lr 0.5, momentum 0.9, weight decay 1e-3; first step: the
+    # buffer is initialised from the gradient), oracle on host copies
+    kw = dict(lr=0.5, momentum=0.9, weight_decay=1e-3)
+    c_ref = torch.from_numpy(cloud0.copy())
+    b_ref = torch.zeros(P)
+    g_ref = torch.empty(P)
+    _oracle_step(ops.ServerStep("fedavg", c_ref, momentum_buf=b_ref, momentum_init=True,
+                                grad_out=g_ref, **kw), torch.from_numpy(avg_ref.copy()))
+    for where in ("host", "hbm"):
+        on = torch.device("cpu") if where == "host" else rk.dev
+        agg = ShardedSerialAggregator(devices=devs)
+        for k in range(K):
+            agg.add("p", src["hbm" if where == "hbm" else "pageable"](k), w[k])
+        cloud = torch.from_numpy(cloud0.copy()).to(on)
+        buf = torch.zeros(P, device=on)
+        grad = torch.empty(P, device=on)
+        agg.pop_step("p", ops.ServerStep("fedavg", cloud, momentum_buf=buf, momentum_init=True,
+                                         grad_out=grad, **kw))
+        record("devices_pop_step_%s_cloud" % where, cloud.cpu().numpy(), c_ref.numpy())
+        record("devices_pop_step_%s_momentum" % where, buf.cpu().numpy(), b_ref.numpy())
+        record("devices_pop_step_%s_grad" % where, grad.cpu().numpy(), g_ref.numpy())
+    torch.cuda.synchronize()
+    return None
 
 
 def fedavg_step(rk, P):
@@ -651,6 +727,178 @@ def fedavg_step(rk, P):
     cloud = torch.zeros(P, dtype=torch.float32, device=rk.dev)
     grad = torch.empty(P, dtype=torch.float32, device=rk.dev)
     return ops.ServerStep("fedavg", cloud, lr=1.0, grad_out=grad), cloud, grad
+
+
+# -- driver-timed side legs (rank 0 at N=1, after the headline) -------------
+H2D_K, H2D_POOL = 64, 8
+
+
+def _sample_cols(P, n=4096, seed=5):
+    import numpy as np
+
+    cols = np.random.default_rng(seed).integers(0, P, size=n)
+    return np.unique(np.concatenate([cols, np.arange(max(0, P - 64), P)]))
+
+
+def h2d_inclusive_leg(rk, P, repeats=3):
+    """The round the north star names second: client vectors arrive as HOST
+    tensors (the reference's CPU-side trainers) and the average returns to
+    the host -- ``SerialAggregator(borrow_host=True).add`` x K then ``pop``
+    into a host tensor, wall clock (perf_counter around synchronised rounds),
+    once from pageable and once from pinned vectors (a pool of H2D_POOL
+    distinct 4P-byte tensors cycled over K adds: PCIe-bound, host memory is
+    read once per client either way).  The PCIe ceiling is one plain pinned
+    H2D copy of the same bytes in this process.  The popped average is
+    checked bitwise against the C oracle on sampled columns, outside the
+    timing.  Reference: training/utils.py:34 (the clone), aggregators.py:
+    23-40, 104-122."""
+    import numpy as np
+    import torch
+
+    from fedsim_amd.utils import SerialAggregator
+    from oracle import ref
+
+    K = H2D_K
+    weights = _weights(K, seed=13)
+    W = sum(weights)
+    g = torch.Generator().manual_seed(29)
+    base = torch.empty(P).normal_(0.0, 0.05, generator=g)
+    pageable = [base + float(k) * 1e-3 for k in range(H2D_POOL)]
+    pinned = [t.pin_memory() for t in pageable]
+    cols = _sample_cols(P)
+    want = ref.reduce(np.stack([pageable[k % H2D_POOL].numpy()[cols] for k in range(K)]),
+                      weights, W=W)
+
+    def one_round(pool):
+        agg = SerialAggregator(borrow_host=True, expected_rows=K)
+        for k in range(K):
+            agg.add("local_params", pool[k % H2D_POOL], weights[k])
+        return agg.pop("local_params")  # host tensor: the D2H completes here
+
+    res = dict(K=K, P=P, pool=H2D_POOL, repeats=repeats, bytes_per_round=4.0 * K * P)
+    checked = True
+    for name, pool in (("pageable", pageable), ("pinned", pinned)):
+        out = one_round(pool)  # warm (ingest ring, staging slots, slab)
+        got = out.numpy()[cols]
+        checked &= bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        secs = []
+        for _ in range(repeats):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = one_round(pool)
+            torch.cuda.synchronize()
+            secs.append(time.perf_counter() - t0)
+        assert out.device.type == "cpu"
+        res[name] = round(4.0 * K * P / (sum(secs) / len(secs)) / 1e9, 2)
+        res[name + "_ms"] = round(sum(secs) / len(secs) * 1e3, 2)
+    dst = torch.empty(P, device=rk.dev)
+    dst.copy_(pinned[0], non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        dst.copy_(pinned[k % H2D_POOL], non_blocking=True)
+    torch.cuda.synchronize()
+    res["ceiling"] = round(4.0 * K * P / (time.perf_counter() - t0) / 1e9, 2)
+    res["ratio"] = {n: round(res[n] / res["ceiling"], 3) for n in ("pageable", "pinned")}
+    res["checked"] = checked
+    res["unit"] = "GB/s"
+    res["check"] = "popped average vs oracle/ref.reduce on %d sampled columns, bitwise" % cols.size
+    res["ceiling_is"] = "plain pinned H2D copies of the same 4KP bytes (torch copy_, one stream)"
+    return res
+
+
+CONFIG_P = 1_085_668  # SimpleCNN2 on CIFAR-100 (BASELINE configs 2 and 3)
+CONFIG_LEGS = (("cfg2_fedavg_K1000", "fedavg", 1000), ("cfg2_fedavg_K10", "fedavg", 10),
+               ("cfg3_adabest_K1000", "adabest", 1000), ("cfg3_adabest_K10", "adabest", 10))
+
+
+def config_legs(rk, steps=20, warmup=2):
+    """BASELINE configs 2 and 3 on the device-resident path: one server
+    round of K client rows of SimpleCNN2 (P = 1,085,668) packed in the
+    column-blocked slab, the exact reduce + divide and the server step --
+    FedAvg (lr 1.0, weights = sample counts U{50..600}) and AdaBest (beta 0.6,
+    lr 1.0, weight 1 per client, avg_params in place) -- through the library's
+    own pop_step policy (_DeviceEntry.pop_step: fused into the last pass when
+    ops.fuse_step_pays, else reduce then fedagg_server_step_f32).  Each is
+    checked first, one round from a known state, against oracle/ref on
+    sampled columns (bitwise), then timed over ``steps`` rounds with HIP
+    events.  Reference: fedavg.py:193-208, adabest.py:172-189."""
+    import numpy as np
+    import torch
+
+    from fedsim_amd import ops
+    from oracle import ref
+
+    P = CONFIG_P
+    C = ops.choose_block_cols(P)
+    cols = _sample_cols(P)
+    cols_t = torch.from_numpy(cols).to(rk.dev)
+    out = {}
+    for name, algo, K in CONFIG_LEGS:
+        Xb = make_pool(rk, K, P, C, seed=41 + K)
+        weights = _weights(K, seed=17) if algo == "fedavg" else [1] * K
+        W = sum(weights)
+        w32 = torch.tensor([ops.fl32(v) for v in weights], dtype=torch.float32, device=rk.dev)
+        g = torch.Generator(device=rk.dev).manual_seed(43)
+        cloud = torch.empty(P, device=rk.dev).normal_(0.0, 0.05, generator=g)
+        aux = torch.empty(P, device=rk.dev).normal_(0.0, 0.05, generator=g) \
+            if algo == "adabest" else None
+        grad = torch.empty(P, device=rk.dev)
+        avg = torch.empty(P, device=rk.dev)
+        step = ops.ServerStep(algo, cloud, lr=1.0, coef=0.6 if algo == "adabest" else 0.0,
+                              aux=aux, grad_out=grad)
+        fused = ops.can_fuse_step(Xb, step) and ops.fuse_step_pays(P, K)
+
+        def one_round():
+            if fused:
+                ops.reduce_blocked_step(Xb, w32, step, W=W)
+            else:
+                ops.reduce_blocked(Xb, w32, avg, W=W, flags=ops.default_flags(C))
+                step.apply(avg)
+
+        c0 = cloud[cols_t].cpu().numpy()
+        a0 = aux[cols_t].cpu().numpy() if aux is not None else None
+        Xs = Xb[cols_t // C, :, cols_t % C].T.contiguous().cpu().numpy()  # [K, cols]
+        one_round()
+        avg_ref = ref.reduce(Xs, weights, W=W)
+        if algo == "fedavg":
+            want = dict(cloud=ref.fedavg_sgd(avg_ref, c0, 1.0))
+        else:
+            c_ref, ap_ref = ref.adabest_sgd(avg_ref, c0, a0, 0.6, 1.0)
+            want = dict(cloud=c_ref, aux=ap_ref)
+        got = dict(cloud=cloud[cols_t].cpu().numpy())
+        if aux is not None:
+            got["aux"] = aux[cols_t].cpu().numpy()
+        checked = all(np.array_equal(got[k].view(np.uint32), want[k].view(np.uint32))
+                      for k in want)
+        for _ in range(warmup):
+            one_round()
+        marks = []
+        for _ in range(steps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            one_round()
+            e1.record()
+            marks.append((e0, e1))
+        torch.cuda.synchronize()
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in marks) / steps
+        # algorithmic bytes: client rows + weights + per column the step's
+        # operands (cloud r/w, grad w; AdaBest's avg_params r/w) and, split,
+        # the stored average's write + read
+        per_col = 12.0 + (8.0 if algo == "adabest" else 0.0) + (0.0 if fused else 8.0)
+        alg = 4.0 * K * P + 4.0 * K + per_col * P
+        out[name] = dict(algo=algo, K=K, P=P, C=C, weights="sample counts U{50..600}"
+                         if algo == "fedavg" else "1 per client", lr=1.0,
+                         beta=0.6 if algo == "adabest" else None,
+                         path="fused" if fused else "split", steps=steps,
+                         ms=round(ms, 4), GBps=round(4.0 * K * P / ms / 1e6, 1),
+                         alg_bytes=alg, frac=round(alg / ms / 1e6 / PEAK_HBM_GBPS, 4),
+                         checked=checked,
+                         check="%d sampled columns vs oracle/ref, bitwise (%s)" % (
+                             cols.size, ", ".join(sorted(want))))
+        del Xb
+    return out
 
 
 # -- param: the headline round ---------------------------------------------
@@ -851,7 +1099,8 @@ def _main(a, quiet):
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={rk.world}")
     clock = KernelClock(rk)
     ar_ms = []
-    selftest = None if a.no_selftest else multi_gpu_selftest(rk, a.selftest_fault_rank)
+    selftest = None if a.no_selftest else multi_gpu_selftest(rk, a.selftest_fault_rank,
+                                                             a.selftest_fault_devices)
     if a.mode == "param":
         step, info, total_bytes, keep = setup_param(a, rk, clock)
     else:
@@ -931,6 +1180,13 @@ def _main(a, quiet):
                      "process group")
     del keep, step
     if not rk.rehearsal:
+        rk.torch.cuda.empty_cache()
+    if rk.rank == 0 and rk.world == 1 and not rk.rehearsal and a.mode == "param" \
+            and not a.no_side_legs:
+        t0 = time.perf_counter()
+        result["h2d_inclusive"] = h2d_inclusive_leg(rk, a.P)
+        result["configs"] = config_legs(rk)
+        result["side_legs_s"] = round(time.perf_counter() - t0, 2)
         rk.torch.cuda.empty_cache()
     if rk.rank == 0 and rk.world == 1 and not a.no_cpu_baseline and not rk.rehearsal:
         result["cpu_baseline"] = cpu_baseline(a.P, a.cpu_baseline_seconds)

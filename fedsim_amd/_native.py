@@ -23,10 +23,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
 
 # Must match include/fedagg.h
-ABI_VERSION = 4  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
+ABI_VERSION = 5  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
 #                 3: the rejected flat-load / LDS-weight flag bits refused;
 #                 4: + fedagg_finalize_f64, fedagg_reduce_rows_ref (fp64 / bf16 /
-#                    fp16 keys of the generic aggregator)
+#                    fp16 keys of the generic aggregator);
+#                 5: + fedagg_rows_plan (which kernel a borrowed-rows call takes)
 FEDAGG_INIT = 0x1
 FEDAGG_FINALIZE = 0x2
 FEDAGG_NT = 0x4
@@ -45,6 +46,15 @@ FEDAGG_POOL_PLANES = 0x1000000
 FEDAGG_CONV_MAXPOOL2 = 0x2000000
 FEDAGG_CONV_POOL_PAD1 = 0x4000000
 FEDAGG_EINVAL = -22
+# fedagg_rows_plan kinds
+FEDAGG_ROWS_NARROW1 = 1
+FEDAGG_ROWS_NARROW2 = 2
+FEDAGG_ROWS_NARROW4 = 3
+FEDAGG_ROWS_WIDE = 4
+FEDAGG_ROWS_TILE4x8 = 5
+FEDAGG_ROWS_TILE8x4 = 6
+FEDAGG_ROWS_SPLITK = 7
+FEDAGG_ROWS_FLAT = 8
 
 FEDAGG_ALGO_FEDAVG = 0
 FEDAGG_ALGO_ADABEST = 1
@@ -109,6 +119,10 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+    ),
+    "fedagg_rows_plan": (
+        ctypes.c_int,
+        [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
     ),
     "fedagg_reduce_f32": (
         ctypes.c_int,

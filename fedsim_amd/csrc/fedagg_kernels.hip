@@ -3375,6 +3375,31 @@ hipError_t launch_rows_ref(const void* const* rows, const void* w, int64_t B, in
   return launch_rows_ref_tile<R, VW, 8, 1>(rows, w, B, P, acc_in, out, init, body, st);
 }
 
+// Which kernel fedagg_reduce_rows_f32 launches (host-side decision; the
+// values are FEDAGG_ROWS_* of include/fedagg.h).  ``vec_ok``: out / acc_in
+// are 16-B aligned and FEDAGG_SCALAR is clear; ``max_vw``: the most columns
+// per lane P and the operands allow.
+int rows_plan(int64_t P, int64_t B, int flags, bool vec_ok, int max_vw) {
+  if (!row_fits_descriptor(P)) return FEDAGG_ROWS_FLAT;  // P = 2^30: flat loads
+  if (fast_split(flags, P)) return FEDAGG_ROWS_SPLITK;
+  // 16-B rows with no tuning field set: wide per-row tiles
+  // (k_reduce_rows_ref<RefF32>, one wave = 8 or 4 KiB of each row per visit)
+  // while the launch keeps kRefMinBlocks workgroups -- 6.0-6.1 -> 6.5-6.7
+  // TB/s at 16-100 MB rows, bitwise the narrow kernel's sums (round 5,
+  // profiles/r05p/, r05u/).  Any explicit tuning field (a forced mapping,
+  // k-unroll, slots per lane or block size: an A/B caller asking for one
+  // kernel) keeps the column kernels it names.
+  constexpr int kTuningFields =
+      FEDAGG_MAP_MASK | FEDAGG_UNROLL_MASK | FEDAGG_VPT_MASK | FEDAGG_BS_MASK;
+  if (B > 0 && vec_ok && max_vw == 4 && (flags & kTuningFields) == 0) {
+    if (rows_ref_blocks(P / 4, 8) >= kRefMinBlocks) return FEDAGG_ROWS_TILE4x8;
+    if (rows_ref_blocks(P / 4, 4) >= kRefMinBlocks) return FEDAGG_ROWS_TILE8x4;
+  }
+  // misaligned rows take the one-column-per-lane kernel whatever the mapping
+  const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
+  return vw ? FEDAGG_ROWS_NARROW1 + (vw == 2) + 2 * (vw == 4) : FEDAGG_ROWS_WIDE;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -3439,38 +3464,47 @@ int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B, 
                          ? 1
                          : max_cols_per_lane(P, {out, init ? nullptr : acc_in});
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (!row_fits_descriptor(P)) {  // P = 2^30: flat loads, one column per lane
-    const EpiStore st{out};
-    return static_cast<int>(
-        (flags & FEDAGG_NT)
-            ? launch_narrow_t<8, 1, true>(NarrowTableFlat{rows}, w, B, P, acc_in, st, W32, flags, s)
-            : launch_narrow_t<8, 1, false>(NarrowTableFlat{rows}, w, B, P, acc_in, st, W32, flags,
-                                           s));
-  }
-  if (const int S = fast_split(flags, P))
-    return static_cast<int>(launch_splitk(NarrowTable{rows, table_row_bytes(P)}, S, w, B, P,
-                                          acc_in, EpiStore{out}, W32, flags, s));
-  // 16-B rows with the default column mapping: wide per-row tiles
-  // (k_reduce_rows_ref<RefF32>, one wave = 8 or 4 KiB of each row per visit)
-  // while the launch keeps kRefMinBlocks workgroups -- 6.0-6.1 -> 6.5-6.7
-  // TB/s at 16-100 MB rows, bitwise the narrow kernel's sums (round 5,
-  // profiles/r05p/, r05u/).  A forced mapping keeps the narrow kernels.
-  if (B > 0 && vec_ok && max_vw == 4 && (flags & FEDAGG_MAP_MASK) == 0) {
-    const bool fin = (flags & FEDAGG_FINALIZE) != 0;
-    const auto rt = reinterpret_cast<const void* const*>(rows);
-    if (rows_ref_blocks(P / 4, 8) >= kRefMinBlocks)
+  const bool fin = (flags & FEDAGG_FINALIZE) != 0;
+  const auto rt = reinterpret_cast<const void* const*>(rows);
+  switch (rows_plan(P, B, flags, vec_ok, max_vw)) {
+    case FEDAGG_ROWS_FLAT: {
+      const EpiStore st{out};
+      return static_cast<int>(
+          (flags & FEDAGG_NT)
+              ? launch_narrow_t<8, 1, true>(NarrowTableFlat{rows}, w, B, P, acc_in, st, W32, flags,
+                                            s)
+              : launch_narrow_t<8, 1, false>(NarrowTableFlat{rows}, w, B, P, acc_in, st, W32,
+                                             flags, s));
+    }
+    case FEDAGG_ROWS_SPLITK:
+      return static_cast<int>(launch_splitk(NarrowTable{rows, table_row_bytes(P)},
+                                            fast_split(flags, P), w, B, P, acc_in, EpiStore{out},
+                                            W32, flags, s));
+    case FEDAGG_ROWS_TILE4x8:
       return static_cast<int>(
           launch_rows_ref_tile<RefF32, 4, 4, 8>(rt, w, B, P, acc_in, out, init, P, s, W32, fin));
-    if (rows_ref_blocks(P / 4, 4) >= kRefMinBlocks)
+    case FEDAGG_ROWS_TILE8x4:
       return static_cast<int>(
           launch_rows_ref_tile<RefF32, 4, 8, 4>(rt, w, B, P, acc_in, out, init, P, s, W32, fin));
+    case FEDAGG_ROWS_WIDE:
+      return static_cast<int>(dispatch_reduce(RowsTableBuf{rows, table_row_bytes(P)}, w, B, P,
+                                              acc_in, out, W32, flags, s));
+    default: {
+      const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
+      return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B,
+                                                  P, acc_in, out, W32, flags, s));
+    }
   }
-  const int vw = vec_ok ? narrow_vw(flags, P, B, max_vw) : 1;
-  if (vw)
-    return static_cast<int>(launch_narrow_store(NarrowTable{rows, table_row_bytes(P)}, vw, w, B, P,
-                                                acc_in, out, W32, flags, s));
-  return static_cast<int>(dispatch_reduce(RowsTableBuf{rows, table_row_bytes(P)}, w, B, P, acc_in,
-                                          out, W32, flags, s));
+}
+
+int fedagg_rows_plan(int64_t P, int64_t B, int flags, int aligned16, int* kind) {
+  if (P < 0 || B < 0 || !kind) return FEDAGG_EINVAL;
+  const bool vec_ok = aligned16 && !(flags & FEDAGG_SCALAR);
+  const int max_vw = (flags & FEDAGG_SCALAR) ? 1
+                     : aligned16             ? max_cols_per_lane(P, {})
+                                             : max_cols_per_lane(P, {reinterpret_cast<void*>(4)});
+  *kind = rows_plan(P, B, flags, vec_ok, max_vw);
+  return 0;
 }
 
 int fedagg_reduce_blocked_f32(const float* Xb, int64_t Kcap, int64_t C, const float* w,

@@ -81,6 +81,22 @@ def column_mapping(P: int, flags: int = 0, max_vw: int = 4, B: int = 1000):
     return ("wide", None) if vw.value == 0 else (f"narrow{vw.value}", u.value)
 
 
+_ROWS_KINDS = {1: "narrow1", 2: "narrow2", 3: "narrow4", 4: "wide", 5: "tile4x8",
+               6: "tile8x4", 7: "splitk", 8: "flat"}
+
+
+def rows_plan(P: int, B: int, flags: int = 0, aligned: bool = True) -> str:
+    """The kernel fedagg_reduce_rows_f32 launches for B borrowed rows x P
+    columns under ``flags`` (fedagg_rows_plan; host-side): ``"tile4x8"`` /
+    ``"tile8x4"`` (the wide per-row tiles of the default flags), ``"narrow1"``
+    / ``"narrow2"`` / ``"narrow4"`` / ``"wide"`` (the column kernels a tuning
+    field names), ``"splitk"`` (FEDAGG_FAST) or ``"flat"``."""
+    kind = ctypes.c_int()
+    check(_native.load().fedagg_rows_plan(P, B, flags, 1 if aligned else 0, ctypes.byref(kind)),
+          "fedagg_rows_plan")
+    return _ROWS_KINDS[kind.value]
+
+
 def choose_block_cols(P: int) -> int:
     """Widest column block that still yields >= ~8 workgroups per CU (the
     sweeps: C=4096 best at P=25M, C=1024 best at P=1.09M)."""

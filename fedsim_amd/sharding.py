@@ -202,7 +202,7 @@ class _ShardEntry(_TensorEntry):
             return super().takes(value, weight)
         return (isinstance(value, torch.Tensor) and value.dtype == self.dtype
                 and value.device == self.out_device and tuple(value.shape) == self.shape
-                and _ref_weight(weight))
+                and not value.requires_grad and _ref_weight(weight))
 
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
@@ -462,7 +462,7 @@ class ShardedSerialAggregator(SerialAggregator):
             return None
         if (isinstance(value, torch.Tensor) and value.dim() > 0 and value.device.type == "cuda"
                 and value.dtype in _RefDeviceEntry.DTYPES and _ref_weight(weight)
-                and type(value) is torch.Tensor):
+                and type(value) is torch.Tensor and not value.requires_grad):
             return _ShardEntry(self, value, ref=True)
         return None
 
@@ -696,6 +696,29 @@ def _meta(x):
     return x
 
 
+def _src_type(value) -> Optional[str]:
+    """Where an N-d message tensor was produced ("cuda" / "cpu"; a stand-in
+    knows its owner's), None for anything else."""
+    if isinstance(value, RemoteRow):
+        return value.src_type
+    if isinstance(value, torch.Tensor) and value.dim() > 0:
+        return value.device.type
+    return None
+
+
+def _check_same_device(sum_meta, sum_type: str, value) -> None:
+    """The reference's ``sum_v + new_v`` (aggregators.py:38,40) raises for an
+    N-d running sum and an N-d value on different devices; the replicated
+    meta arithmetic cannot see devices, so every rank checks the recorded
+    source types instead and raises together, the key unchanged."""
+    vt = _src_type(value)
+    if (vt is not None and isinstance(sum_meta, torch.Tensor) and sum_meta.dim() > 0
+            and vt != sum_type):
+        raise RuntimeError(
+            "Expected all tensors to be on the same device: a %s value added to a key "
+            "whose running sum is on %s" % (vt, sum_type))
+
+
 class _ClientShardRef(_TensorEntry):
     """A tensor key of a client-sharded round that keeps the reference's
     arithmetic (aggregators.py:17-40): non-fp32 values (an fp64 / bf16
@@ -722,9 +745,11 @@ class _ClientShardRef(_TensorEntry):
         self.owners = []  # ranks holding rows, in arrival order (one run each)
         self.after = []   # meta of the running sum after each owner's run
         self.dev = agg._reduce_device()
+        self.src_type = src_type
         self.out_device = self.dev if src_type == "cuda" else torch.device("cpu")
 
     def add(self, value, weight) -> None:
+        _check_same_device(self.meta, self.src_type, value)
         meta, new_w = reference_add((self.meta, self.cur_w), _meta(value), weight)
         remote = isinstance(value, RemoteRow)
         owner = value.owner if remote else self.agg.rank
@@ -1037,9 +1062,12 @@ class ClientShardedSerialAggregator(SerialAggregator):
         src = value.src_type if isinstance(value, RemoteRow) else \
             value.device.type if tensor else "cpu"
         if isinstance(e, _ClientShardEntry) and _kernel_value(value, weight) and \
-                tuple(value.shape) == e.shape:
+                tuple(value.shape) == e.shape and src == e.src_type:
             e.add(value, weight)
             return
+        if isinstance(e, _ClientShardEntry) and tensor and src != e.src_type:
+            # the reference's sum_v + new_v raises; the key stays as it was
+            _check_same_device(torch.empty(e.shape, device="meta"), e.src_type, value)
         if e is None and _kernel_value(value, weight):
             e = _ClientShardEntry(self, value.shape, src)
             e._key = key

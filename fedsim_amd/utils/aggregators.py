@@ -313,11 +313,18 @@ class _TensorEntry(object):
     cur_w = 0
     dev = None
     shape = ()
+    out_device = None  # the first value's device (None: not tracked)
 
     def takes(self, value, weight) -> bool:
         """Whether this entry adds (value, weight) itself; otherwise the key
-        leaves it for the reference's arithmetic (SerialAggregator.add)."""
-        return _kernel_value(value, weight) and tuple(value.shape) == self.shape
+        leaves it for the reference's arithmetic (SerialAggregator.add).  A
+        value on another device than the key's first value is left to that
+        arithmetic too, where ``sum_v + new_v`` raises as in the reference
+        (aggregators.py:38,40) and the key stays as it was: the rule is
+        relative to the delivery device, not the compute device (host values
+        into HIP shards are one device)."""
+        return (_kernel_value(value, weight) and tuple(value.shape) == self.shape
+                and (self.out_device is None or value.device == self.out_device))
 
 
 class _DeviceEntry(_TensorEntry):
@@ -458,8 +465,15 @@ class _DeviceEntry(_TensorEntry):
         return row
 
     def release(self) -> None:
-        """Drop the slab; SlabRows still alive keep a copy of their row."""
-        self._copies_issued()
+        """Drop the slab; SlabRows still alive keep a copy of their row.  A
+        failed staging put is not raised again here (add and the reductions
+        raise it): a cleanup must not hide the first error.  The copy stream
+        is drained instead, so no DMA still writes into the freed slab."""
+        try:
+            self._copies_issued()
+        except BaseException:  # noqa: BLE001 -- the entry's own calls raise it
+            self.copy_event = None
+            self.agg._ingest(self.dev).stream.synchronize()
         if self.copy_event is not None:  # the slab is read by the copy stream until then
             self.copy_event.synchronize()
             self.copy_event = None
@@ -700,9 +714,13 @@ def _kernel_weight(weight) -> bool:
 
 def _kernel_value(value, weight) -> bool:
     """Whether (value, weight) is the fp32 kernel path's: an fp32 N-d tensor
-    and a real scalar weight."""
+    that does not require grad, and a real scalar weight.  A value that
+    requires grad keeps the reference's arithmetic: its ``value * weight``
+    (aggregators.py:21) carries the autograd graph into the sum and the
+    quotient, which a kernel row cannot."""
     return (isinstance(value, torch.Tensor) and value.dim() > 0
-            and value.dtype == torch.float32 and _kernel_weight(weight))
+            and value.dtype == torch.float32 and not value.requires_grad
+            and _kernel_weight(weight))
 
 
 def reference_add(pair, value, weight):
@@ -729,14 +747,14 @@ def reference_quotient(v, w):
     promotion (an integer sum divides into the default float dtype), the
     division is IEEE true division in ATen's opmath type (f64 for fp64, f32
     for fp32 / fp16 / bf16) by the weight rounded to that type, then rounded
-    to the quotient's dtype."""
+    to the quotient's dtype.  A sum that requires grad gets the reference's
+    autograd node (``v / w``) holding these bits."""
     if not (isinstance(v, torch.Tensor) and v.device.type == "cuda" and v.dim() > 0
             and not v.is_complex()):
         return v / w
     if isinstance(w, torch.Tensor):
-        # a 0-dim host weight (a tensor-valued running weight) is first cast
-        # to the common dtype, as ATen's TensorIterator does
-        if w.dim() != 0 or w.device.type != "cpu" or w.is_complex():
+        if (w.dim() != 0 or w.device.type != "cpu" or w.is_complex()
+                or w.requires_grad):
             return v / w
     elif not isinstance(w, (int, float, np.integer, np.floating)):
         return v / w
@@ -744,17 +762,32 @@ def reference_quotient(v, w):
     if not out.is_floating_point:
         out = torch.get_default_dtype()  # true division of integers
     if isinstance(w, torch.Tensor):
-        w = w.to(out).item()
+        if out in (torch.float16, torch.bfloat16):
+            # ATen CPU's reduced-float divide by a CPU scalar reads the
+            # scalar's ORIGINAL value into opmath f32 (div_true_kernel,
+            # original_scalar_value<opmath_t>): finalize applies fl32 to it
+            w = w.item()
+        else:
+            # otherwise the 0-dim weight is first cast to the common dtype,
+            # as ATen's TensorIterator does
+            w = w.to(out).item()
+    x = v.detach()
     if out == torch.float64:
-        x = v.to(torch.float64).contiguous()
+        x = x.to(torch.float64).contiguous()
         q = ops.finalize_f64(x if x.data_ptr() % 16 == 0 else x.clone(), w)
     elif out in _F32_OPMATH:
-        x = v.to(torch.float32).contiguous()
+        x = x.to(torch.float32).contiguous()
         q = ops.finalize(x if x.data_ptr() % 16 == 0 else x.clone(), w,
                          out=torch.empty(x.shape, dtype=torch.float32, device=x.device))
     else:
         return v / w
-    return q.view(v.shape).to(out)
+    q = q.view(v.shape).to(out)
+    if v.requires_grad:
+        g = v / w  # the reference's graph node (DivBackward saves v and w, not g)
+        with torch.no_grad():
+            g.copy_(q)
+        return g
+    return q
 
 
 def _ref_weight(weight) -> bool:
@@ -794,7 +827,7 @@ class _RefDeviceEntry(_TensorEntry):
     def takes(self, value, weight) -> bool:
         return (isinstance(value, torch.Tensor) and value.dtype == self.dtype
                 and value.device == self.dev and tuple(value.shape) == self.shape
-                and _ref_weight(weight))
+                and not value.requires_grad and _ref_weight(weight))
 
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
@@ -914,7 +947,7 @@ class SerialAggregator(object):
         sharded aggregators keep such keys on the host path)."""
         if (isinstance(value, torch.Tensor) and value.dim() > 0 and value.device.type == "cuda"
                 and value.dtype in _RefDeviceEntry.DTYPES and _ref_weight(weight)
-                and type(value) is torch.Tensor):
+                and type(value) is torch.Tensor and not value.requires_grad):
             return _RefDeviceEntry(value, self._opts)
         return None
 

@@ -65,8 +65,8 @@ extern "C" {
    flat-load and LDS-weight A/B switches, measured and rejected) are no
    longer accepted (FEDAGG_EINVAL); 4: + fedagg_finalize_f64 and
    fedagg_reduce_rows_ref (the dtype-generic SerialAggregator's fp64 / bf16 /
-   fp16 keys) */
-#define FEDAGG_ABI_VERSION 4
+   fp16 keys); 5: + fedagg_rows_plan */
+#define FEDAGG_ABI_VERSION 5
 
 /* flags for the reduce entry points */
 #define FEDAGG_INIT      0x1  /* ignore acc_in: start from +0.0f (first batch of a round) */
@@ -171,10 +171,28 @@ int fedagg_reduce_f32(const float* X, int64_t ldx, const float* w, int64_t B,
  * already resident in HBM without packing them into a slab first.
  * The table lives in device memory and is not inspected on the host: the
  * caller must pass FEDAGG_SCALAR unless every rows[k] is 16-byte aligned.
+ * With no tuning field set (FEDAGG_MAP/UNROLL/VPT/BS_MASK all zero) and
+ * 16-byte operands, large P takes the wide per-row tiles; any tuning field
+ * selects the narrow / wide column kernels those bits name.
  */
 int fedagg_reduce_rows_f32(const float* const* rows, const float* w, int64_t B,
                            int64_t P, const float* acc_in, float* out, float W32,
                            int flags, void* stream);
+
+/*
+ * Which kernel fedagg_reduce_rows_f32 launches for B rows x P columns under
+ * ``flags`` when every operand is 16-byte aligned (aligned16 != 0) or not
+ * (host-side decision, no device access): *kind = one of FEDAGG_ROWS_*.
+ */
+#define FEDAGG_ROWS_NARROW1 1 /* one column per lane                        */
+#define FEDAGG_ROWS_NARROW2 2 /* two columns per lane                       */
+#define FEDAGG_ROWS_NARROW4 3 /* four columns per lane                      */
+#define FEDAGG_ROWS_WIDE    4 /* f32x4-slot column kernels (FEDAGG_MAP = 1) */
+#define FEDAGG_ROWS_TILE4x8 5 /* wide per-row tile, 4 rows x 8 KiB          */
+#define FEDAGG_ROWS_TILE8x4 6 /* wide per-row tile, 8 rows x 4 KiB          */
+#define FEDAGG_ROWS_SPLITK  7 /* FEDAGG_FAST split-K (small P, reordered)   */
+#define FEDAGG_ROWS_FLAT    8 /* P * 4 >= 4 GiB: flat loads                 */
+int fedagg_rows_plan(int64_t P, int64_t B, int flags, int aligned16, int* kind);
 
 /*
  * Same reduction over a COLUMN-BLOCKED slab: columns are cut into blocks of C

@@ -41,7 +41,7 @@ def test_header_declares_the_abi():
     fns = header_functions()
     assert fns == sorted([
         "fedagg_abi_version", "fedagg_strerror", "fedagg_column_mapping", "fedagg_reduce_f32",
-        "fedagg_reduce_rows_f32",
+        "fedagg_reduce_rows_f32", "fedagg_rows_plan",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_pack_segments_f32",
         "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_teacher_conv2d_f32",
         "fedagg_conv_stage", "fedagg_conv_order", "fedagg_conv_pool_fusable", "fedagg_pool_output",
@@ -202,6 +202,35 @@ def test_column_mapping_decision():
     assert ops.column_mapping(7, ops.tuning_flags(mapping="narrow1", unroll=16)) == ("narrow1", 16)
     # unroll selectors the narrow kernels do not build fall back to the default
     assert ops.column_mapping(199_210, ops.tuning_flags(unroll=4)) == ("narrow1", 8)
+
+
+def test_rows_plan_decision():
+    """fedagg_rows_plan: the borrowed-rows call takes the wide per-row tiles
+    only under the default flags (NT / INIT / FINALIZE allowed); any tuning
+    field -- a forced mapping, k-unroll, slots per lane, block size -- keeps
+    the column kernel it names, so an A/B caller measures what it asked for
+    (advisor, round 5).  Host-side, no device needed."""
+    from fedsim_amd import _native, ops
+
+    base = _native.FEDAGG_NT | _native.FEDAGG_INIT | _native.FEDAGG_FINALIZE
+    assert ops.rows_plan(25_000_000, 1000) == "tile4x8"
+    assert ops.rows_plan(25_000_000, 1000, base) == "tile4x8"
+    assert ops.rows_plan(3_000_004, 11) == "tile8x4"
+    assert ops.rows_plan(1_500_000, 9) == "narrow2"        # too few workgroups for a tile
+    assert ops.rows_plan(199_210, 1000) == "narrow1"
+    assert ops.rows_plan(25_000_001, 1000) == "narrow1"    # odd P: no 16-B vectors
+    assert ops.rows_plan(25_000_000, 1000, aligned=False) == "narrow1"
+    assert ops.rows_plan(25_000_000, 0) == "narrow4"        # no rows: the tiles need one
+    assert ops.rows_plan(25_000_000, 1000, _native.FEDAGG_SCALAR) == "narrow1"
+    for tuned, want in ((ops.tuning_flags(mapping="narrow2"), "narrow2"),
+                        (ops.tuning_flags(mapping="narrow4"), "narrow4"),
+                        (ops.tuning_flags(mapping="wide"), "wide"),
+                        (ops.tuning_flags(unroll=4), "narrow2"),
+                        (ops.tuning_flags(vpt=2), "narrow2"),
+                        (ops.tuning_flags(bs=512), "narrow2")):
+        assert ops.rows_plan(25_000_000, 1000, base | tuned) == want, hex(tuned)
+    assert ops.rows_plan(4096, 1000, ops.tuning_flags(fast=True)) == "splitk"
+    assert ops.rows_plan(1 << 30, 2) == "flat"
 
 
 def test_conv_and_pool_host_side_shapes(lib):

@@ -53,6 +53,8 @@ def _selftest_ok(d, world):
     st = d["multi_gpu_selftest"]
     assert st["ok"] and st["world"] == world, st
     assert set(st["checks"]) == SELFTEST_CHECKS
+    # rank 0's one-process devices=[...] check needs several GPUs: recorded skip
+    assert st["devices"] == "skipped: no HIP device (CPU rehearsal)"
     for name, c in st["checks"].items():
         assert c["ok"], (name, c)
         assert c["bitwise"] == (name != "client_allreduce")
@@ -70,6 +72,23 @@ def test_selftest_mismatch_fails_every_rank():
     assert len(lines) == 1
     st = json.loads(lines[0])["multi_gpu_selftest"]
     assert st["ok"] is False and st["checks"]["param_sharded_step"]["ok"] is True  # rank 0's
+
+
+@pytest.mark.parametrize("gpus", [1, 3])
+def test_selftest_devices_failure_fails_every_rank(gpus):
+    """A failing devices_* check (rank 0's one-process multi-GPU mode, injected
+    here since the rehearsal has no GPU) fails the self-test on every rank:
+    the run exits 3 instead of timing, the line names the check."""
+    r = _bench("--gpus", str(gpus), "--rehearsal-stub", "tests.bench_stub:reduce", "--K", "4",
+               "--P", "256", "--steps", "1", "--warmup", "1", "--selftest-fault-devices",
+               timeout=180)
+    assert r.returncode == 3, r.stderr[-2000:]
+    assert "multi-GPU self-test FAILED" in r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    st = json.loads(lines[0])["multi_gpu_selftest"]
+    assert st["ok"] is False and st["checks"]["devices_get_pageable"]["ok"] is False
+    assert all(c["ok"] for n, c in st["checks"].items() if not n.startswith("devices_"))
 
 
 def test_launcher_rank_failure_fails_run():

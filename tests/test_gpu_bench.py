@@ -73,3 +73,17 @@ def test_one_gpu_line_carries_selftest(launch):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     _selftest_ok(d, 1, "nccl" if launch == "torchrun_rccl" else None)
+    # one GPU on the box: rank 0's devices=[...] check records its skip
+    assert d["multi_gpu_selftest"]["devices"] == "skipped: 1 device"
+    # the N=1 side legs: the host-to-host round and BASELINE configs 2 / 3,
+    # each checked against the oracle before it is timed
+    h = d["h2d_inclusive"]
+    assert h["checked"] is True and h["P"] == 2_000_000 and h["K"] == 64
+    assert 0 < h["pageable"] and 0 < h["pinned"] and 0 < h["ceiling"]
+    cfg = d["configs"]
+    assert set(cfg) == {"cfg2_fedavg_K1000", "cfg2_fedavg_K10", "cfg3_adabest_K1000",
+                        "cfg3_adabest_K10"}
+    for name, c in cfg.items():
+        assert c["checked"] is True and c["ms"] > 0 and 0 < c["frac"] < 1.2, (name, c)
+    assert cfg["cfg2_fedavg_K1000"]["path"] == "split"  # ops.fuse_step_pays at 1.09 M x 1000
+    assert cfg["cfg2_fedavg_K10"]["path"] == "fused"
