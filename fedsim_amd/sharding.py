@@ -164,8 +164,8 @@ def weights_fp32(weights: Sequence, device) -> torch.Tensor:
 # plugin surface: a parameter-sharded SerialAggregator
 # ---------------------------------------------------------------------------
 from .utils.aggregators import (  # noqa: E402
-    SerialAggregator, _DeviceEntry, _hip_device, _kernel_value, _ref_weight, _RefDeviceEntry,
-    _TensorEntry, reference_add, reference_quotient)
+    SerialAggregator, _deliver_to, _DeviceEntry, _hip_device, _kernel_value, _ref_weight,
+    _RefDeviceEntry, _TensorEntry, reference_add, reference_quotient)
 
 
 def _group_rank_world(group):
@@ -239,8 +239,7 @@ class _ShardEntry(_TensorEntry):
         return full
 
     def _deliver(self, t: torch.Tensor) -> torch.Tensor:
-        t = t.view(self.shape)
-        return t if t.device == self.out_device else t.to(self.out_device)
+        return _deliver_to(t.view(self.shape), self.out_device)
 
     # -- reference semantics --------------------------------------------------
     def get(self) -> torch.Tensor:
@@ -666,8 +665,7 @@ class _ClientShardEntry(_TensorEntry):
         return self.agg.divide(s, self.cur_w)
 
     def _deliver(self, t: torch.Tensor) -> torch.Tensor:
-        t = t.view(self.shape)
-        return t if t.device == self.out_device else t.to(self.out_device)
+        return _deliver_to(t.view(self.shape), self.out_device)
 
     def get(self) -> torch.Tensor:
         return self._deliver(self._average())
@@ -791,7 +789,7 @@ class _ClientShardRef(_TensorEntry):
 
     def _deliver(self, t):
         if isinstance(t, torch.Tensor) and t.dim() > 0 and t.device != self.out_device:
-            t = t.to(self.out_device)
+            t = _deliver_to(t, self.out_device)
         return t
 
     def _weighted(self) -> bool:

@@ -86,6 +86,57 @@ def _fl32(x) -> float:
     return _F32.unpack(_F32.pack(x))[0]
 _STAGING_SLOTS = 3
 
+# Host threads of one staging copy (pageable client vector -> pinned slot):
+# one memmove ran at 35 GB/s on the MI355X box's EPYC host, four at 72 --
+# above PCIe's 52-57, so the DMA, not the copy, paces a handed-over round
+# (tools/probe_h2d.py, profiles/r06b/).  Chunks below 8 MB stay on one thread.
+_STAGE_THREADS = max(1, int(os.environ.get("FEDSIM_AMD_STAGE_THREADS", 4)))
+_STAGE_CHUNK_MIN = 8 << 20
+_stage_pool: Optional[ThreadPoolExecutor] = None
+
+
+def _staging_copy(dst: int, src: int, nbytes: int) -> None:
+    """memmove(dst, src, nbytes) split over up to _STAGE_THREADS threads
+    (ctypes' memmove releases the GIL while it copies)."""
+    global _stage_pool
+    n = min(_STAGE_THREADS, max(1, nbytes // _STAGE_CHUNK_MIN))
+    if n <= 1:
+        ctypes.memmove(dst, src, nbytes)
+        return
+    if _stage_pool is None:
+        _stage_pool = ThreadPoolExecutor(max_workers=_STAGE_THREADS - 1,
+                                         thread_name_prefix="fedsim-stage")
+    step = (nbytes // n + 4095) & ~4095
+    futs = [_stage_pool.submit(ctypes.memmove, dst + i * step, src + i * step,
+                               min(step, nbytes - i * step))
+            for i in range(1, n) if i * step < nbytes]
+    ctypes.memmove(dst, src, min(step, nbytes))
+    for f in futs:
+        f.result()
+
+
+def to_host(t: torch.Tensor) -> torch.Tensor:
+    """A HIP tensor delivered to the host in page-locked memory: one DMA at
+    PCIe rate.  A pageable destination ran at 6.7 GB/s on the MI355X box
+    (first-touch faults of fresh pages behind the runtime's staging), a
+    pinned one at 56.8 GB/s (tools/probe_h2d.py, profiles/r06b/): for the
+    25 M-parameter average, 15 ms against 1.8 ms.  The result is an ordinary
+    CPU tensor (``is_pinned()`` is True); torch's host allocator recycles the
+    block once it is freed."""
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return h
+
+
+def _deliver_to(t: torch.Tensor, device: torch.device) -> torch.Tensor:
+    """``t.to(device)`` with the D2H leg through pinned memory."""
+    if t.device == device:
+        return t
+    if device.type == "cpu" and t.device.type == "cuda" and not t.requires_grad:
+        return to_host(t)
+    return t.to(device)
+
 
 def _hip_device(value: torch.Tensor, device) -> torch.device:
     if device is not None:
@@ -184,10 +235,10 @@ class _Ingest(object):
         else:
             host = self._slot(self.hbufs, i, P, pin_memory=True)
             if version is not None and src.dtype == torch.float32 and src.is_contiguous():
-                # on the worker thread, while the next client trains: one
-                # single-threaded memcpy (torch's copy_ would start its own
-                # OpenMP team and contend with the training threads)
-                ctypes.memmove(host.data_ptr(), src.data_ptr(), 4 * P)
+                # on the worker thread, while the next client trains: a few
+                # memmove threads (torch's copy_ would start its own OpenMP
+                # team and contend with the training threads)
+                _staging_copy(host.data_ptr(), src.data_ptr(), 4 * P)
             else:
                 host.copy_(src)
             self._check_version(src, version)  # not changed while it was copied
@@ -636,10 +687,7 @@ class _DeviceEntry(_TensorEntry):
         return not (self.cur_w is None or self.cur_w == 0)
 
     def _deliver(self, t: torch.Tensor) -> torch.Tensor:
-        t = t.view(self.shape)
-        if self.out_device != t.device:
-            t = t.to(self.out_device)  # D2H (or peer) copy; synchronises for CPU
-        return t
+        return _deliver_to(t.view(self.shape), self.out_device)  # D2H: pinned, synchronised
 
     def get(self) -> torch.Tensor:
         self._flush(final_W=None)

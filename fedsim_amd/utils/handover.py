@@ -58,7 +58,16 @@ _OPEN = []  # the driver's open rounds (nested drivers: innermost last)
 
 def hand_over(t):
     """Declare that ``t`` is given away to the server (see the module
-    docstring); returns ``t``.  A no-op outside a driver round."""
+    docstring); returns ``t``.  A no-op outside a driver round.
+
+    What is detected afterwards is torch's version counter: an in-place
+    torch op on ``t`` (or a view of it) between this call and the read
+    makes the reduction raise.  Writes that bypass the counter are NOT
+    detected -- ``t.data.copy_(...)``, writes through ``t.numpy()`` or a
+    DLPack / ``__array_interface__`` alias, or a kernel writing the storage
+    by pointer -- and the aggregator then reads the changed values.  A
+    producer that keeps a handle it may write that way must not hand the
+    tensor over (only the library's own ``sgd_update`` calls this today)."""
     if _OPEN and isinstance(t, torch.Tensor):
         _OPEN[-1].tokens[id(t)] = (weakref.ref(t), t._version)
     return t
