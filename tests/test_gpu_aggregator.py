@@ -264,9 +264,12 @@ def test_full_size_properties(dev):
 
 @pytest.mark.parametrize("max_rows", [1, 2, 3, 7, 64])
 def test_ingest_ring_bitwise(max_rows, dev):
-    """Many adds through a small ring: host (pageable + pinned) and device
-    sources interleaved, sources mutated right after add, ring growth, wrap and
-    double-buffered drains — result equals the oracle bitwise."""
+    """Many adds through a small ring: host sources (pageable + pinned
+    interleaved) into one key and HIP sources into another, sources mutated
+    right after add, ring growth, wrap and double-buffered drains -- results
+    equal the oracle bitwise.  A vector from the other side added to either
+    key raises, as the reference's ``sum_v + new_v`` does, and changes
+    nothing (fedsim/utils/aggregators.py:38,40)."""
     from fedsim_amd.utils import SerialAggregator
 
     K, P = 29, 10_007
@@ -276,21 +279,26 @@ def test_ingest_ring_bitwise(max_rows, dev):
     scratch = torch.empty(P)
     pinned = torch.empty(P).pin_memory()
     for k in range(K):
-        if k % 3 == 0:
+        if k % 2 == 0:
             src = scratch
             src.copy_(torch.from_numpy(X[k]))
-        elif k % 3 == 1:
+        else:
             src = pinned
             src.copy_(torch.from_numpy(X[k]))
-        else:
-            src = torch.from_numpy(X[k].copy()).to(dev)
         agg.add("p", src, w[k])
-        if k % 3 != 2:
-            src.fill_(float("nan"))  # the snapshot must already be taken
+        src.fill_(float("nan"))  # the snapshot must already be taken
+        agg.add("d", torch.from_numpy(X[k].copy()).to(dev), w[k])
         if k == K // 2:
+            for key, other in (("p", torch.ones(P, device=dev)), ("d", torch.ones(P))):
+                with pytest.raises(RuntimeError, match="same device"):
+                    agg.add(key, other, 3)
             mid = agg.get("p")  # non-destructive read in the middle of the stream
             exp_mid = ref.reduce(X[: k + 1], w[: k + 1], W=sum(w[: k + 1]))
             np.testing.assert_array_equal(bits(mid.numpy()), bits(exp_mid))
+    assert agg.get_weight("p") == agg.get_weight("d") == sum(w)
     out = agg.pop("p")
-    assert out.device.type == "cpu"  # first value was a host tensor
+    assert out.device.type == "cpu"  # the values were host tensors
     np.testing.assert_array_equal(bits(out.numpy()), bits(ref.reduce(X, w, W=sum(w))))
+    outd = agg.pop("d")
+    assert outd.device == dev
+    np.testing.assert_array_equal(bits(outd.cpu().numpy()), bits(ref.reduce(X, w, W=sum(w))))

@@ -43,8 +43,10 @@ def test_borrowed_rows_bitwise(P, max_rows, dev):
 
 
 def test_borrow_interleaved_with_host_and_unaligned_sources(dev):
-    """Host adds (snapshotted into the slab) and misaligned device views
-    (snapshotted too) between borrowed rows: arrival order is kept."""
+    """Strided device views and misaligned device views (both snapshotted
+    into the slab) between borrowed rows: arrival order is kept.  A host
+    vector added to the HIP key raises as the reference's ``sum_v + new_v``
+    does (aggregators.py:38,40) and leaves the rows as they were."""
     from fedsim_amd.utils import SerialAggregator
 
     K, P = 17, 10_007
@@ -52,9 +54,14 @@ def test_borrow_interleaved_with_host_and_unaligned_sources(dev):
     w = V.client_weights("fednova", K, 9)
     agg = SerialAggregator(borrow=True)
     big = torch.empty(P + 1, device=dev)
+    wide = torch.empty(2 * P, device=dev)
     for k in range(K):
+        if k == 5:
+            with pytest.raises(RuntimeError, match="same device"):
+                agg.add("p", torch.from_numpy(X[k].copy()), w[k])
         if k % 4 == 1:
-            src = torch.from_numpy(X[k].copy())                 # host: slab path
+            wide[::2].copy_(torch.from_numpy(X[k]))            # strided view: slab path
+            src = wide[::2]
         elif k % 4 == 3:
             big[1:].copy_(torch.from_numpy(X[k]))              # 4-B offset view: slab path
             src = big[1:]
@@ -63,6 +70,8 @@ def test_borrow_interleaved_with_host_and_unaligned_sources(dev):
         agg.add("p", src, w[k])
         if k % 4 == 3:
             big.fill_(float("nan"))  # the misaligned view was snapshotted at add
+        if k % 4 == 1:
+            wide.fill_(float("nan"))  # so was the strided one
     out = agg.pop("p")
     np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref.reduce(X, w, W=sum(w))))
 
@@ -470,23 +479,32 @@ def test_handed_over_host_rows_are_staged_after_add(dev):
     """borrow_host=True with host vectors (the round driver's aggregator under
     device="cpu"): each handed-over vector is copied into pinned staging and
     DMA'd by the ingest worker after add returns (while the next client
-    trains), in arrival order, interleaved with HBM rows; the round is the
-    oracle's bit for bit."""
+    trains), in arrival order, interleaved with the HBM rows of another key
+    (borrowed); both rounds are the oracle's bit for bit.  An HBM vector
+    added to the host key raises (the reference's ``sum_v + new_v``)."""
     from fedsim_amd.utils import SerialAggregator
 
     K, P = 23, 600_001  # above _ASYNC_STAGE_MIN: the worker stages them
     X = V.client_rows("realistic", K, P, 8)
     w = V.client_weights("fedavg", K, 8)
     agg = SerialAggregator(borrow=True, borrow_host=True, max_rows=5)
+    sel = [k for k in range(K) if k % 5 == 4]
     for k in range(K):
         src = torch.from_numpy(X[k].copy())
-        if k % 5 == 4:
-            src = src.to(dev)
         agg.add("p", src, w[k])
         del src
+        if k in sel:
+            agg.add("d", torch.from_numpy(X[k].copy()).to(dev), w[k])
+        if k == 9:
+            with pytest.raises(RuntimeError, match="same device"):
+                agg.add("p", torch.from_numpy(X[k].copy()).to(dev), w[k])
     out = agg.pop("p")
     assert out.device.type == "cpu"
     np.testing.assert_array_equal(bits(out.numpy()), bits(ref.reduce(X, w, W=sum(w))))
+    ws = [w[k] for k in sel]
+    outd = agg.pop("d")
+    assert outd.device == dev
+    np.testing.assert_array_equal(bits(outd.cpu().numpy()), bits(ref.reduce(X[sel], ws, W=sum(ws))))
 
 
 def test_small_handed_over_host_rows_are_staged_at_add(dev):

@@ -108,20 +108,26 @@ def test_fused_step_random(dev, r, algo, m, lr):
 @SETTINGS
 @given(rounds(max_k=24, max_p=3000), st.integers(1, 9))
 def test_aggregator_random_stream(dev, r, max_rows):
-    """add() x K through a small ring (host and HBM sources), then pop()."""
+    """add() x K through a small ring, host sources into one key and HBM
+    sources into another (one key holds one device, as the reference's
+    running sum does), then pop()."""
     from fedsim_amd.utils import SerialAggregator
 
     X, w = r
     agg = SerialAggregator(max_rows=max_rows)
     for k in range(X.shape[0]):
         src = torch.from_numpy(X[k].copy())
-        agg.add("p", src.to(dev) if k % 2 else src, w[k])
+        agg.add("h", src, w[k])
+        agg.add("d", src.to(dev), w[k])
     if X.shape[0] == 0:
-        assert "p" not in agg
+        assert "h" not in agg and "d" not in agg
         return
-    got = agg.pop("p")
     W = sum(w)  # add() does not skip zero weights; W == 0 -> pop returns the raw sum
-    same(got.cpu().numpy(), ref.reduce(X, w, W=W if W else None))
+    want = ref.reduce(X, w, W=W if W else None)
+    got_h, got_d = agg.pop("h"), agg.pop("d")
+    assert got_h.device.type == "cpu" and got_d.device == dev
+    same(got_h.numpy(), want)
+    same(got_d.cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("C", [1024, 4096])
@@ -212,10 +218,13 @@ class _TwoParams(torch.nn.Module):
        st.sampled_from(["pop", "fedavg", "adabest"]))
 def test_mixed_sources_random_stream(dev, r, max_rows, borrow, kinds, final):
     """Every way a client vector reaches the aggregator, interleaved at
-    random in one round: pageable host, pinned host (overwritten right after
-    add), HBM (borrowed or packed), a model vectorized into a reserved slab
-    row, and a reservation whose client never arrives; a mid-stream get; then
-    pop or the fused pop + server step.  Bitwise vs the oracle."""
+    random in one round: pageable host and pinned host (overwritten right
+    after add) into the host key "h"; HBM (borrowed or packed), a model
+    vectorized into a reserved slab row, and a reservation whose client never
+    arrives into the HIP key "p" (one key holds one device, as the
+    reference's running sum does; an add across them raises, checked once);
+    a mid-stream get; then pop or the fused pop + server step.  Bitwise vs
+    the oracle."""
     from fedsim_amd import ops
     from fedsim_amd.utils import SerialAggregator, vectorize_module
 
@@ -224,6 +233,7 @@ def test_mixed_sources_random_stream(dev, r, max_rows, borrow, kinds, final):
     agg = SerialAggregator(max_rows=max_rows, borrow=borrow)
     model = _TwoParams(P, dev)
     pinned = torch.empty(P).pin_memory()
+    on_host = []
     for k in range(K):
         kind = kinds[k]
         if kind == 4:
@@ -239,15 +249,35 @@ def test_mixed_sources_random_stream(dev, r, max_rows, borrow, kinds, final):
         else:
             model.load(torch.from_numpy(X[k]).to(dev))
             src = vectorize_module(model, out=agg.reserve("p", P, dev))
-        agg.add("p", src, w[k])
+        on_host.append(kind in (0, 1))
+        key = "h" if on_host[-1] else "p"
+        other = "p" if on_host[-1] else "h"
+        if k == K // 2 and other in agg:  # once per round: the other key refuses it
+            with pytest.raises(RuntimeError, match="same device"):
+                agg.add(other, src, w[k])
+        agg.add(key, src, w[k])
         if kind == 1:
             pinned.fill_(float("nan"))
         if k == K // 2:
-            W2 = sum(w[: k + 1])
-            same(agg.get("p").cpu().numpy(), ref.reduce(X[: k + 1], w[: k + 1], W=W2 or None))
+            for kk, host in (("h", True), ("p", False)):
+                sel = [i for i in range(k + 1) if on_host[i] == host]
+                if sel:
+                    ws = [w[i] for i in sel]
+                    same(agg.get(kk).cpu().numpy(), ref.reduce(X[sel], ws, W=sum(ws) or None))
     if K == 0:
+        assert "p" not in agg and "h" not in agg
+        return
+    hsel = [i for i in range(K) if on_host[i]]
+    if hsel:
+        ws = [w[i] for i in hsel]
+        got = agg.pop("h")
+        assert got.device.type == "cpu"
+        same(got.numpy(), ref.reduce(X[hsel], ws, W=sum(ws) or None))
+    dsel = [i for i in range(K) if not on_host[i]]
+    if not dsel:
         assert "p" not in agg
         return
+    X, w = X[dsel], [w[i] for i in dsel]
     W = sum(w)
     avg = ref.reduce(X, w, W=W if W else None)
     if final == "pop":

@@ -193,9 +193,11 @@ def test_sharded_round_loop_two_ranks_on_one_gpu(round_arrays):
 
 @pytest.mark.parametrize("borrow", [False, True])
 def test_sharded_aggregator_sources_one_rank(borrow, pg):
-    """Pageable, pinned and HBM-resident client vectors through the sharded
-    aggregator (RCCL, one rank): get mid-stream, pop and pop_step with a
-    momentum SGD step, bitwise vs the oracle."""
+    """Pageable and pinned host client vectors into one key and HBM-resident
+    ones into another through the sharded aggregator (RCCL, one rank): get
+    mid-stream, pop, and pop_step with a momentum SGD step, bitwise vs the
+    oracle.  A key holds one device, as the reference's running sum does:
+    a host vector added to the HIP key raises and changes nothing."""
     from fedsim_amd import ops
     from fedsim_amd.sharding import ShardedSerialAggregator
 
@@ -203,6 +205,10 @@ def test_sharded_aggregator_sources_one_rank(borrow, pg):
     K, P = 29, 100_003
     X = V.client_rows("realistic", K, P, 5)
     w = V.client_weights("fedavg", K, 5)
+    hk = [k for k in range(K) if k % 3 != 2]
+    dk = [k for k in range(K) if k % 3 == 2]
+    wh, wd = [w[k] for k in hk], [w[k] for k in dk]
+    avg_h, avg_d = ref.reduce(X[hk], wh, W=sum(wh)), ref.reduce(X[dk], wd, W=sum(wd))
     for final in ("pop", "step"):
         agg = ShardedSerialAggregator(borrow=borrow)
         pinned = torch.empty(P).pin_memory()
@@ -214,22 +220,28 @@ def test_sharded_aggregator_sources_one_rank(borrow, pg):
                 src.copy_(torch.from_numpy(X[k]))
             else:
                 src = torch.from_numpy(X[k].copy()).to(dev)
-            agg.add("p", src, w[k])
+            agg.add("d" if k % 3 == 2 else "p", src, w[k])
             if k % 3 == 1:
                 src.fill_(float("nan"))  # snapshot already taken
             if k == K // 2:
+                with pytest.raises(RuntimeError, match="same device"):
+                    agg.add("d", torch.from_numpy(X[k].copy()), w[k])
+                sel = [i for i in hk if i <= k]
+                ws = [w[i] for i in sel]
                 mid = agg.get("p")
-                exp_mid = ref.reduce(X[: k + 1], w[: k + 1], W=sum(w[: k + 1]))
-                np.testing.assert_array_equal(bits(mid.cpu().numpy()), bits(exp_mid))
-        avg_ref = ref.reduce(X, w, W=sum(w))
+                np.testing.assert_array_equal(bits(mid.cpu().numpy()),
+                                              bits(ref.reduce(X[sel], ws, W=sum(ws))))
+        outd = agg.pop("d")
+        assert outd.device == dev
+        np.testing.assert_array_equal(bits(outd.cpu().numpy()), bits(avg_d))
         if final == "pop":
             out = agg.pop("p")
-            assert out.device.type == "cpu"  # the first value was a host tensor
-            np.testing.assert_array_equal(bits(out.numpy()), bits(avg_ref))
+            assert out.device.type == "cpu"  # the values were host tensors
+            np.testing.assert_array_equal(bits(out.numpy()), bits(avg_h))
             continue
         cloud0 = V.cloud_vector(P, 6)
         st = ref.ServerState("fedavg", cloud0, dict(lr=0.3, momentum=0.9))
-        st.step(avg_ref)
+        st.step(avg_h)
         cloud = torch.from_numpy(cloud0.copy()).to(dev)
         grad = torch.empty_like(cloud)
         buf = torch.empty_like(cloud)
@@ -284,9 +296,12 @@ def test_single_process_device_shards_round_loop(run, device, round_arrays):
 
 
 def test_single_process_device_shards_sources():
-    """Host (pageable / pinned) and HBM vectors through three device shards:
-    get mid-stream, pop to the host, and pop_step with a momentum SGD step on
-    a host-resident cloud, bitwise vs the oracle."""
+    """Host (pageable / pinned) vectors into one key and HBM vectors into
+    another through three device shards: get mid-stream, pop to the host /
+    the GPU, and pop_step with a momentum SGD step on a host-resident cloud,
+    bitwise vs the oracle.  Host values into HIP shards are one device (the
+    first value's); an HBM vector added to the host key raises, as the
+    reference's host sum would, and the reverse."""
     from fedsim_amd import ops
     from fedsim_amd.sharding import ShardedSerialAggregator
 
@@ -294,6 +309,10 @@ def test_single_process_device_shards_sources():
     K, P = 17, 300_007
     X = V.client_rows("realistic", K, P, 15)
     w = V.client_weights("fedavg", K, 15)
+    hk = [k for k in range(K) if k % 3 != 2]
+    dk = [k for k in range(K) if k % 3 == 2]
+    wh, wd = [w[k] for k in hk], [w[k] for k in dk]
+    avg_h, avg_d = ref.reduce(X[hk], wh, W=sum(wh)), ref.reduce(X[dk], wd, W=sum(wd))
     for final in ("pop", "step"):
         agg = ShardedSerialAggregator(devices=[dev] * 3, borrow=True)
         for k in range(K):
@@ -302,20 +321,28 @@ def test_single_process_device_shards_sources():
                 src = src.pin_memory()
             elif k % 3 == 2:
                 src = src.to(dev)
-            agg.add("p", src, w[k])
+            agg.add("d" if k % 3 == 2 else "p", src, w[k])
             if k == 8:
+                with pytest.raises(RuntimeError, match="same device"):
+                    agg.add("p", torch.from_numpy(X[k].copy()).to(dev), w[k])
+                with pytest.raises(RuntimeError, match="same device"):
+                    agg.add("d", torch.from_numpy(X[k].copy()), w[k])
+                sel = [i for i in hk if i <= k]
+                ws = [w[i] for i in sel]
                 mid = agg.get("p")
-                np.testing.assert_array_equal(
-                    bits(mid.cpu().numpy()), bits(ref.reduce(X[:9], w[:9], W=sum(w[:9]))))
-        avg_ref = ref.reduce(X, w, W=sum(w))
+                np.testing.assert_array_equal(bits(mid.cpu().numpy()),
+                                              bits(ref.reduce(X[sel], ws, W=sum(ws))))
+        outd = agg.pop("d")
+        assert outd.device == dev
+        np.testing.assert_array_equal(bits(outd.cpu().numpy()), bits(avg_d))
         if final == "pop":
             out = agg.pop("p")
             assert out.device.type == "cpu"
-            np.testing.assert_array_equal(bits(out.numpy()), bits(avg_ref))
+            np.testing.assert_array_equal(bits(out.numpy()), bits(avg_h))
             continue
         cloud0 = V.cloud_vector(P, 16)
         st = ref.ServerState("fedavg", cloud0, dict(lr=0.3, momentum=0.9))
-        st.step(avg_ref)
+        st.step(avg_h)
         cloud = torch.from_numpy(cloud0.copy())
         grad, buf = torch.empty_like(cloud), torch.empty_like(cloud)
         agg.pop_step("p", ops.ServerStep("fedavg", cloud, lr=0.3, momentum=0.9,

@@ -70,9 +70,11 @@ def test_pack_layout_is_parameters_to_vector(scale):
 
 
 def test_reserved_rows_reduce_bitwise_with_other_sources():
-    """Slab rows, borrowed HBM tensors and host tensors interleaved, a
-    reservation that is never added (a diverged client), and a small ring
-    that wraps: the average equals the oracle's over the added vectors."""
+    """Slab rows and borrowed HBM tensors interleaved (host tensors of the
+    same clients into a host key alongside), a reservation that is never
+    added (a diverged client), and a small ring that wraps: each average
+    equals the oracle's over its added vectors.  A host vector added to the
+    HIP key raises, as the reference's ``sum_v + new_v`` does."""
     from fedsim_amd.utils import vectorize_module
 
     K = 23
@@ -86,13 +88,19 @@ def test_reserved_rows_reduce_bitwise_with_other_sources():
     for borrow, max_rows in ((True, 4096), (False, 3), (True, 2)):
         agg = _agg(borrow=borrow, max_rows=max_rows)
         added = []
+        on_host = []
         kept = []
         for k in range(K):
             if k % 4 == 0:
                 agg.reserve("p", P, DEV)  # reserved, then the client diverged
             if k % 3 == 0:
-                val = vecs[k].cpu()
-            elif k % 3 == 1:
+                agg.add("h", vecs[k].cpu(), w[k])
+                on_host.append(k)
+                if "p" in agg:
+                    with pytest.raises(RuntimeError, match="same device"):
+                        agg.add("p", vecs[k].cpu(), w[k])
+                continue
+            if k % 3 == 1:
                 val = vecs[k].clone()
             else:
                 val = vectorize_module(models[k], out=agg.reserve("p", P, DEV))
@@ -101,10 +109,12 @@ def test_reserved_rows_reduce_bitwise_with_other_sources():
             agg.add("p", val, w[k])
             added.append(k)
             assert "p" in agg
-        out = agg.pop("p")
-        X = np.stack([vecs[k].cpu().numpy() for k in added])
-        exp = ref.reduce(X, [w[k] for k in added], W=sum(w[k] for k in added))
-        np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(exp))
+        for key, rows in (("p", added), ("h", on_host)):
+            out = agg.pop(key)
+            assert out.device.type == ("cuda" if key == "p" else "cpu")
+            X = np.stack([vecs[k].cpu().numpy() for k in rows])
+            exp = ref.reduce(X, [w[k] for k in rows], W=sum(w[k] for k in rows))
+            np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(exp))
         for row, v in kept:  # reused rows / released slab: the value is kept
             assert torch.equal(row.view(torch.int32), v.view(torch.int32))
 
