@@ -525,6 +525,35 @@ def test_small_handed_over_host_rows_are_staged_at_add(dev):
     np.testing.assert_array_equal(bits(agg.pop("l").numpy()), bits(ref.reduce(Xl, w, W=sum(w))))
 
 
+def test_release_after_failed_put_keeps_the_first_error(dev):
+    """An entry whose staging put failed (a handed-over host vector changed
+    before the worker copied it) can still be released: release() drains the
+    copy stream and frees the slab without raising again (advisor, round 5),
+    and the key's own reads keep raising the first error."""
+    import threading
+
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _ingest_for
+
+    agg = SerialAggregator(borrow=True, borrow_host=True)
+    gate = threading.Event()
+    _ingest_for(dev).pool.submit(gate.wait)
+    t = torch.ones(1 << 20)
+    agg.add("p", t, 1)
+    t.mul_(2)
+    gate.set()
+    e = agg._members["p"]
+    with pytest.raises(RuntimeError, match="modified in place"):
+        e._copies_issued()
+    e.release()  # no second raise; the slab is dropped
+    assert e.slab is None
+    e.release()  # idempotent
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.get("p")
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.pop("p")
+
+
 def test_handed_over_host_row_mutated_in_place_raises(dev):
     """A handed-over host vector changed in place before the ingest worker
     copied it is refused at the reduction (held back here so the change comes

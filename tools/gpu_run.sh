@@ -31,7 +31,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-PMC_ARGS="--steps 3 --warmup 1 --no-cpu-baseline"
+PMC_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-side-legs"
 
 pmc() {  # pmc <counters> <dir> <cmd...>
   local c=$1 d=$2
