@@ -11,6 +11,7 @@
 #   test=<spec>      pytest -m gpu on one file / node id (tests/<spec>)
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (the driver's default line)
+#   benchmode=<mode> python bench.py --mode strong|allreduce (configs 4 / 5 at N=1)
 #   rocprof          rocprofv3 --kernel-trace --stats of bench.py (10 steps)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes of the bench kernel + the
 #                    tools/pmc_calib calibration -> pmc_traffic.json (with the
@@ -55,6 +56,10 @@ step() {
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench)
       timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    benchmode=*)
+      arg=${s#benchmode=}
+      timeout -k 10 600 python bench.py --mode $arg --no-cpu-baseline > "$OUT/bench_$arg.json" \
+        2> "$OUT/bench_$arg.err" ;;
     rocprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$TAG -o bench \
         -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.log" 2>&1 \
