@@ -15,11 +15,15 @@ INTEGRATION.md §3: the reference resolver's own ``path/file:Class`` form
 pointing at ``fedsim_amd/plugins.py`` (no patch at all), or one line
 adding ``fedsim_amd.distributed.centralized.training`` to the module list.
 
-Parity: the reference resolver cannot be imported here (it imports skopt,
-which is absent), so this restatement is "parity unpinned" -- it is checked
-against the reference's documented grammar in tests/test_cli_resolution.py.
+Parity: pinned to the reference's own resolver.  tools/gen_golden_cli.py
+runs fedsim_cli/utils.py's ``ingest_fed_context`` in the build container
+(skopt, absent here and used only for fed-tune's search spaces, replaced by
+a stub that records their arguments) on 16 token lists; this restatement
+gives the same algorithm entries and raises the same exceptions
+(tests/test_cli_golden.py, tests/golden/cli_resolution.json).
 Hyper-parameter search spaces (``lr:Real:0-1``, used only by fed-tune) are
-parsed into ``SearchSpace`` tuples instead of ``eval``'d skopt objects.
+parsed into ``SearchSpace`` tuples instead of ``eval``'d skopt objects, with
+the same kind and arguments.
 """
 from __future__ import annotations
 

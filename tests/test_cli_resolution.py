@@ -4,9 +4,9 @@
 :221-230 (base-class argument guard), :235-236 (partial binding) and the
 instantiation of fedsim_cli/fed_learn.py:372-389.
 
-PARITY UNPINNED: the reference resolver imports skopt, which is not
-installed, so it cannot be run here to produce fixtures; these tests pin the
-grammar the reference's own code and tests (tests/test_cli.py:14-40) use."""
+These tests check the grammar and the instantiation; the resolver's
+outputs are pinned to the reference's own resolver in tests/test_cli_golden.py
+(fixtures from tools/gen_golden_cli.py)."""
 import os
 from collections import OrderedDict
 from functools import partial
