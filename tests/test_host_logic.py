@@ -486,3 +486,27 @@ def test_hand_over_round_scope_releases_tokens():
         u = torch.ones(4)
         assert take_token(u) is False
     assert not _OPEN and take_token(u) is None
+
+
+@pytest.mark.parametrize("nbytes", [0, 1, 4095, 4096, 4097, 3 * 4096 + 5, 1 << 16, (1 << 16) + 12])
+@pytest.mark.parametrize("threads", [1, 2, 3, 4])
+def test_staging_copy_splits_exactly(monkeypatch, nbytes, threads):
+    """The ingest worker's multi-threaded staging copy (aggregators.
+    _staging_copy) writes exactly the source bytes for any size and thread
+    count: page-rounded chunks, a short last chunk, sizes below one page,
+    and nothing past the end of the destination."""
+    import numpy as np
+
+    from fedsim_amd.utils import aggregators as A
+
+    monkeypatch.setattr(A, "_STAGE_CHUNK_MIN", 4096)
+    monkeypatch.setattr(A, "_STAGE_THREADS", threads)
+    monkeypatch.setattr(A, "_stage_pool", None)
+    rng = np.random.default_rng(nbytes + threads)
+    src = rng.integers(0, 256, size=max(nbytes, 1), dtype=np.uint8)
+    dst = np.full(nbytes + 64, 0xA5, dtype=np.uint8)  # a guard band after the copy
+    A._staging_copy(dst.ctypes.data, src.ctypes.data, nbytes)
+    assert np.array_equal(dst[:nbytes], src[:nbytes])
+    assert (dst[nbytes:] == 0xA5).all()
+    if A._stage_pool is not None:
+        A._stage_pool.shutdown()
