@@ -278,3 +278,94 @@ def test_hip_quotient_tensor_weights_reduced_floats():
             assert q.dtype == want.dtype and q.device == dev, (dt, w)
             assert np.array_equal(q.cpu().view(-1).view(torch.uint8).numpy(),
                                   want.view(-1).view(torch.uint8).numpy()), (dt, w)
+
+
+# ---------------------------------------------------------------------------
+# random sessions: every mix of dtype, device, shape, requires_grad and
+# weight kind the reference's add accepts or refuses
+def _session_strategy():
+    from hypothesis import strategies as st
+
+    value = st.fixed_dictionaries({
+        "dtype": st.sampled_from(["f32", "f32", "f32", "f64", "bf16"]),
+        "dev": st.sampled_from(["cuda", "cuda", "cpu"]),
+        "dim": st.sampled_from([1, 1, 1, 0]),
+        "rg": st.sampled_from([False, False, False, True]),
+        "seed": st.integers(0, 10_000),
+    })
+    weight = st.one_of(st.integers(1, 600), st.sampled_from([0.25, 2.5, 7.3, 0]),
+                       st.sampled_from(["t301", "t2", "none"]))
+    step = st.one_of(
+        st.tuples(st.just("add"), st.sampled_from(["p", "q"]), value, weight),
+        st.tuples(st.sampled_from(["get", "get_sum", "get_weight", "pop", "in"]),
+                  st.sampled_from(["p", "q"])),
+    )
+    return st.lists(step, min_size=1, max_size=10)
+
+
+_DT = {"f32": torch.float32, "f64": torch.float64, "bf16": torch.bfloat16}
+
+
+def _materialize(steps):
+    """Hypothesis steps -> replay() steps (values built fresh per replay)."""
+    out = []
+    for st_ in steps:
+        if st_[0] != "add":
+            out.append(st_)
+            continue
+        _, key, v, w = st_
+        dt = _DT[v["dtype"]]
+        n = 1031 if v["dim"] else None
+        rg = v["rg"]
+
+        def make(v=v, dt=dt, n=n, rg=rg):
+            g = torch.Generator().manual_seed(v["seed"])
+            t = (torch.randn(n if n else (), generator=g, dtype=torch.float64) * 0.7).to(dt)
+            t = t.to("cuda:0" if v["dev"] == "cuda" else "cpu")
+            return t.requires_grad_(True) if rg else t
+        if w == "t301":
+            w = torch.tensor(301.0)
+        elif w == "t2":
+            w = torch.tensor(2, dtype=torch.int64)
+        elif w == "none":
+            w = None
+        out.append(("add", key, make, w))
+    return out
+
+
+@pytest.mark.gpu
+def test_random_sessions_match_reference_gpu():
+    """Hypothesis-generated sessions over two keys: fp32 / fp64 / bf16 values
+    on the host or in HBM, N-d or 0-dim, with or without requires_grad,
+    Python / 0-dim tensor / zero / None weights, reads interleaved, through
+    a small ring (max_rows=2).  The drop-in's transcript must equal the
+    reference restatement's on the same tensors."""
+    from hypothesis import HealthCheck, given, settings
+
+    from fedsim_amd.utils import SerialAggregator
+
+    assert torch.cuda.is_available()
+
+    seen = {"sessions": 0, "raise": 0, "grad": 0, "kernel_key": 0, "host_result": 0}
+
+    @settings(max_examples=300, deadline=None, derandomize=True,
+              suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+    @given(_session_strategy())
+    def run(steps):
+        ms = _materialize(steps)
+        agg = SerialAggregator(max_rows=2)
+        got = replay(agg, ms)
+        assert got == replay(CpuQuotientReference(), ms)
+        text = repr(got)
+        seen["sessions"] += 1
+        seen["raise"] += "'raise'" in text
+        seen["grad"] += "'rg': True" in text
+        seen["host_result"] += "'dev': 'cpu'" in text
+        seen["kernel_key"] += any(type(e).__name__ == "_DeviceEntry"
+                                  for e in agg._members.values())
+
+    run()
+    # the generator reached every regime it is meant to cover
+    assert seen["sessions"] >= 250, seen
+    assert min(seen["raise"], seen["grad"], seen["host_result"], seen["kernel_key"]) >= 10, seen
+    print("random sessions:", seen)
