@@ -45,7 +45,6 @@ add raises.
 """
 from __future__ import annotations
 
-import ctypes
 import os
 import struct
 from collections import deque
@@ -86,31 +85,43 @@ def _fl32(x) -> float:
     return _F32.unpack(_F32.pack(x))[0]
 _STAGING_SLOTS = 3
 
-# Host threads of one staging copy (pageable client vector -> pinned slot):
-# one memmove ran at 35 GB/s on the MI355X box's EPYC host, four at 72 --
-# above PCIe's 52-57, so the DMA, not the copy, paces a handed-over round
-# (tools/probe_h2d.py, profiles/r06b/).  Chunks below 8 MB stay on one thread.
-_STAGE_THREADS = max(1, int(os.environ.get("FEDSIM_AMD_STAGE_THREADS", 4)))
-_STAGE_CHUNK_MIN = 8 << 20
+# How the ingest worker copies a handed-over pageable vector into pinned
+# staging: "auto", "torch" (torch's multi-threaded copy_) or "memmove<N>" (N
+# threads of ctypes memmove).  Interleaved on one box (tools/ab_staging.py,
+# profiles/r06o/): below 32 MB torch's copy_ wins (a K=10 x 4.3 MB round
+# 1.39-1.41 ms against 1.92-1.98 for four memmoves, 2.0-2.3 for one); at
+# 100 MB four memmoves keep the round at the link (53.2-53.4 GB/s against
+# 43-46 for torch's copy_, whose 16 threads take the host memory bandwidth
+# the concurrent DMA reads from).  "auto" takes each below / from 32 MB.
+_STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
+_STAGE_SPLIT_MIN = 32 << 20
 _stage_pool: Optional[ThreadPoolExecutor] = None
 
 
-def _staging_copy(dst: int, src: int, nbytes: int) -> None:
-    """memmove(dst, src, nbytes) split over up to _STAGE_THREADS threads
-    (ctypes' memmove releases the GIL while it copies)."""
+def _staging_copy(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """dst.copy_(src) for a pinned fp32 slot and a source of its size, by
+    _STAGE_COPY's method."""
     global _stage_pool
-    n = min(_STAGE_THREADS, max(1, nbytes // _STAGE_CHUNK_MIN))
-    if n <= 1:
-        ctypes.memmove(dst, src, nbytes)
+    how = _STAGE_COPY
+    if how == "auto":
+        how = "memmove4" if 4 * src.numel() >= _STAGE_SPLIT_MIN else "torch"
+    if how == "torch" or not (src.is_contiguous() and src.dtype == torch.float32):
+        dst.copy_(src)
         return
-    if _stage_pool is None:
-        _stage_pool = ThreadPoolExecutor(max_workers=_STAGE_THREADS - 1,
-                                         thread_name_prefix="fedsim-stage")
+    import ctypes
+
+    n = max(1, int(how[len("memmove"):] or 1))
+    nbytes, d, s = 4 * src.numel(), dst.data_ptr(), src.data_ptr()
+    if n == 1:
+        ctypes.memmove(d, s, nbytes)
+        return
+    if _stage_pool is None or _stage_pool._max_workers < n - 1:
+        _stage_pool = ThreadPoolExecutor(max_workers=n - 1, thread_name_prefix="fedsim-stage")
     step = (nbytes // n + 4095) & ~4095
-    futs = [_stage_pool.submit(ctypes.memmove, dst + i * step, src + i * step,
+    futs = [_stage_pool.submit(ctypes.memmove, d + i * step, s + i * step,
                                min(step, nbytes - i * step))
             for i in range(1, n) if i * step < nbytes]
-    ctypes.memmove(dst, src, min(step, nbytes))
+    ctypes.memmove(d, s, min(step, nbytes))
     for f in futs:
         f.result()
 
@@ -174,7 +185,7 @@ class _Ingest(object):
     trains instead of between the two clients (tools/bench_host_rounds.py:
     0.2-1.5 ms per client on the critical path otherwise).  A handed-over
     vector changed in place (an in-place torch op: its version counter) from
-    ``add`` until its copy has completed -- the memmove into staging, or for
+    ``add`` until its copy has completed -- the copy into staging, or for
     a pinned source the DMA straight from it -- is caught: the counter is
     checked before and after the copy, and the error is raised at the
     round's reduction.  A change after that point cannot alter the row."""
@@ -234,13 +245,12 @@ class _Ingest(object):
             host = src  # DMA straight from the caller's pinned buffer
         else:
             host = self._slot(self.hbufs, i, P, pin_memory=True)
-            if version is not None and src.dtype == torch.float32 and src.is_contiguous():
-                # on the worker thread, while the next client trains: a few
-                # memmove threads (torch's copy_ would start its own OpenMP
-                # team and contend with the training threads)
-                _staging_copy(host.data_ptr(), src.data_ptr(), 4 * P)
-            else:
-                host.copy_(src)
+            # on the ingest worker too, while the next client trains: a
+            # multi-threaded copy (_staging_copy; one memmove ran at 29 GB/s
+            # from cold client memory, tools/probe_put.py, profiles/r06m/),
+            # which meets the clients' training threads for tens of
+            # microseconds per client
+            _staging_copy(host, src)
             self._check_version(src, version)  # not changed while it was copied
         with torch.cuda.stream(self.stream):
             dslot.copy_(host, non_blocking=True)

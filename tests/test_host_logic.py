@@ -488,25 +488,28 @@ def test_hand_over_round_scope_releases_tokens():
     assert not _OPEN and take_token(u) is None
 
 
-@pytest.mark.parametrize("nbytes", [0, 1, 4095, 4096, 4097, 3 * 4096 + 5, 1 << 16, (1 << 16) + 12])
-@pytest.mark.parametrize("threads", [1, 2, 3, 4])
-def test_staging_copy_splits_exactly(monkeypatch, nbytes, threads):
-    """The ingest worker's multi-threaded staging copy (aggregators.
-    _staging_copy) writes exactly the source bytes for any size and thread
-    count: page-rounded chunks, a short last chunk, sizes below one page,
-    and nothing past the end of the destination."""
-    import numpy as np
 
+@pytest.mark.parametrize("how", ["auto", "torch", "memmove1", "memmove3", "memmove4"])
+@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 3 * 1024 + 5, 1 << 14, (1 << 14) + 3])
+def test_staging_copy_is_exact(monkeypatch, how, n):
+    """The ingest worker's staging copy (aggregators._staging_copy) writes
+    exactly the source floats for every method, size and thread split
+    (page-rounded chunks, a short last chunk, sizes below one page) and
+    nothing past the destination slice; strided or non-fp32 sources take
+    torch's copy."""
     from fedsim_amd.utils import aggregators as A
 
-    monkeypatch.setattr(A, "_STAGE_CHUNK_MIN", 4096)
-    monkeypatch.setattr(A, "_STAGE_THREADS", threads)
+    monkeypatch.setattr(A, "_STAGE_COPY", how)
+    monkeypatch.setattr(A, "_STAGE_SPLIT_MIN", 4096)  # "auto" splits from 1024 floats
     monkeypatch.setattr(A, "_stage_pool", None)
-    rng = np.random.default_rng(nbytes + threads)
-    src = rng.integers(0, 256, size=max(nbytes, 1), dtype=np.uint8)
-    dst = np.full(nbytes + 64, 0xA5, dtype=np.uint8)  # a guard band after the copy
-    A._staging_copy(dst.ctypes.data, src.ctypes.data, nbytes)
-    assert np.array_equal(dst[:nbytes], src[:nbytes])
-    assert (dst[nbytes:] == 0xA5).all()
+    g = torch.Generator().manual_seed(n)
+    src = torch.randn(n, generator=g)
+    buf = torch.full((n + 16,), 7.25)
+    A._staging_copy(buf[:n], src)
+    assert torch.equal(buf[:n].view(torch.int32), src.view(torch.int32))
+    assert (buf[n:] == 7.25).all()
+    wide = torch.randn(2 * n + 2, generator=g)
+    A._staging_copy(buf[:n + 1], wide[::2])  # strided source
+    assert torch.equal(buf[:n + 1], wide[::2])
     if A._stage_pool is not None:
         A._stage_pool.shutdown()

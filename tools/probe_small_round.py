@@ -50,11 +50,7 @@ def main():
     ap.add_argument("--P", type=int, default=199_210)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--borrow-host", type=int, default=1)
-    ap.add_argument("--chunk-min", type=int, default=None,
-                    help="override aggregators._STAGE_CHUNK_MIN (bytes per staging thread)")
     a = ap.parse_args()
-    if a.chunk_min is not None:
-        A._STAGE_CHUNK_MIN = a.chunk_min
     dev = torch.device("cuda:0")
     wrap(A._Ingest, "_put_locked", "put")
     wrap(A._DeviceEntry, "_flush", "flush")
@@ -84,7 +80,7 @@ def main():
         if rep >= 3:
             rounds.append((t1 - t0, t2 - t1, t2 - t0))
     med = lambda xs: statistics.median(xs) * 1e6  # noqa: E731
-    out = dict(K=a.K, P=a.P, reps=a.reps, stage_chunk_min=A._STAGE_CHUNK_MIN,
+    out = dict(K=a.K, P=a.P, reps=a.reps,
                receive_us=med([r[0] for r in rounds]), optimize_us=med([r[1] for r in rounds]),
                round_us=med([r[2] for r in rounds]),
                stages_us_per_call={k: med(v) for k, v in T.items()},
