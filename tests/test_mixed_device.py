@@ -196,6 +196,12 @@ def _mixed_scenarios():
                           ("add", "g", _v(77, dtype=torch.bfloat16, dev=D), 5), ("pop", "g")],
         "grad_then_host": [("add", "g", _v(78, rg=True, dev=D), 3),
                            ("add", "g", _v(79, dev=H), 5)] + _reads("g") + [("pop", "g")],
+        # 0-dim HIP sums (a metric kept on the GPU): ATen CPU's quotient bits
+        "hip_0dim_metrics": [("add", "m", lambda: torch.tensor(0.731, device=D), 2.5),
+                             ("add", "m", lambda: torch.tensor(1.9, device=D), 7),
+                             ("add", "d", lambda: torch.tensor(0.1, dtype=torch.float64,
+                                                               device=D), 3)] +
+        _reads("m") + _reads("d") + [("pop", "m"), ("pop", "d")],
         # a whole round's mixed keys, read with pop_all
         "pop_all_mixed": [("add", "local_params", _v(80, dev=D), 37),
                           ("add", "clients.train.loss", lambda: 0.75, 37),
