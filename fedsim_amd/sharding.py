@@ -316,8 +316,22 @@ class _DevicesEntry(_TensorEntry):
         flat = src.reshape(-1)
         for (lo, hi), inner in zip(self.spans, self.inners):
             if inner is not None:
-                inner.add(flat[lo:hi], weight)  # host slices: each GPU's own copy stream
+                with torch.cuda.device(inner.dev):  # its launches: its device current
+                    inner.add(flat[lo:hi], weight)  # host slices: each GPU's own copy stream
         self.cur_w = new_w
+
+    def _each(self, fn):
+        """fn(inner) for every shard, with that shard's GPU as the current
+        device: libfedagg launches on the stream it is handed, and HIP
+        launches go to the current device's queues."""
+        out = []
+        for inner in self.inners:
+            if inner is None:
+                out.append(None)
+                continue
+            with torch.cuda.device(inner.dev):
+                out.append(fn(inner))
+        return out
 
     def _assemble(self, parts, on=None) -> torch.Tensor:
         on = self.out_device if on is None else on
@@ -333,15 +347,13 @@ class _DevicesEntry(_TensorEntry):
         return full
 
     def get(self) -> torch.Tensor:
-        return self._assemble([None if e is None else e.get() for e in self.inners]).view(
-            self.shape)
+        return self._assemble(self._each(lambda e: e.get())).view(self.shape)
 
     def get_sum(self) -> torch.Tensor:
-        return self._assemble([None if e is None else e.get_sum() for e in self.inners]).view(
-            self.shape)
+        return self._assemble(self._each(lambda e: e.get_sum())).view(self.shape)
 
     def pop(self, on_device: bool = False) -> torch.Tensor:
-        parts = [None if e is None else e.pop(on_device=True) for e in self.inners]
+        parts = self._each(lambda e: e.pop(on_device=True))
         return self._assemble(parts).view(self.shape)
 
     def pop_step(self, step: ops.ServerStep) -> None:
@@ -354,19 +366,23 @@ class _DevicesEntry(_TensorEntry):
             if inner is None:
                 continue
             sub = step.narrow(lo, hi)
-            if inner.dev != home:
-                moved = {n: t.to(inner.dev, non_blocking=True) for n, t in sub.operands.items()}
-                local = ops.ServerStep(step.algo, moved.pop("cloud"), **step._scalars, **moved)
-                inner.pop_step(local)
-                back.append((sub, local, inner.dev))
-            else:
-                inner.pop_step(sub)
+            with torch.cuda.device(inner.dev):
+                if inner.dev != home:
+                    moved = {n: t.to(inner.dev, non_blocking=True)
+                             for n, t in sub.operands.items()}
+                    local = ops.ServerStep(step.algo, moved.pop("cloud"), **step._scalars,
+                                           **moved)
+                    inner.pop_step(local)
+                    back.append((sub, local, inner.dev))
+                else:
+                    inner.pop_step(sub)
         for sub, local, dev in back:
             host = home.type == "cpu"
-            for name, t in local.operands.items():
-                sub.operands[name].copy_(t, non_blocking=host)
-            if host:
-                torch.cuda.current_stream(dev).synchronize()
+            with torch.cuda.device(dev):
+                for name, t in local.operands.items():
+                    sub.operands[name].copy_(t, non_blocking=host)
+                if host:
+                    torch.cuda.current_stream(dev).synchronize()
 
 
 class ShardedSerialAggregator(SerialAggregator):

@@ -45,6 +45,7 @@ add raises.
 """
 from __future__ import annotations
 
+import functools
 import os
 import struct
 from collections import deque
@@ -147,6 +148,21 @@ def _deliver_to(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     if device.type == "cpu" and t.device.type == "cuda" and not t.requires_grad:
         return to_host(t)
     return t.to(device)
+
+
+def _on_own_device(fn):
+    """Run an entry method with the entry's GPU as the current device:
+    libfedagg launches on the stream it is handed, and HIP launches go to the
+    current device's queues (a key on cuda:1 used while cuda:0 is current,
+    or one shard of a single-process multi-GPU key)."""
+    @functools.wraps(fn)
+    def on_device(self, *args, **kwargs):
+        idx = getattr(self.dev, "index", None)
+        if idx is None or torch.cuda.current_device() == idx:
+            return fn(self, *args, **kwargs)
+        with torch.cuda.device(idx):
+            return fn(self, *args, **kwargs)
+    return on_device
 
 
 def _hip_device(value: torch.Tensor, device) -> torch.device:
@@ -513,6 +529,7 @@ class _DeviceEntry(_TensorEntry):
             ev.record(torch.cuda.current_stream(self.dev))
             self.wait_before_copy = ev
 
+    @_on_own_device
     def reserve(self) -> SlabRow:
         """The next ring row, as a SlabRow a client can vectorize its model
         into (slab_rows.py); ``add`` of that row commits it in place."""
@@ -525,6 +542,7 @@ class _DeviceEntry(_TensorEntry):
         self.rows.track(row)
         return row
 
+    @_on_own_device
     def release(self) -> None:
         """Drop the slab; SlabRows still alive keep a copy of their row.  A
         failed staging put is not raised again here (add and the reductions
@@ -543,6 +561,7 @@ class _DeviceEntry(_TensorEntry):
         self.slab = None
 
     # -- reference semantics -------------------------------------------------
+    @_on_own_device
     def add(self, value: torch.Tensor, weight) -> None:
         if _KEEPALIVE:  # an earlier round's borrowed rows, once it has run
             _prune_keepalive_at_add()
@@ -699,16 +718,19 @@ class _DeviceEntry(_TensorEntry):
     def _deliver(self, t: torch.Tensor) -> torch.Tensor:
         return _deliver_to(t.view(self.shape), self.out_device)  # D2H: pinned, synchronised
 
+    @_on_own_device
     def get(self) -> torch.Tensor:
         self._flush(final_W=None)
         if not self._weighted():
             return self._deliver(self.acc.clone())
         return self._deliver(ops.finalize(self.acc, self.cur_w))
 
+    @_on_own_device
     def get_sum(self) -> torch.Tensor:
         self._flush(final_W=None)
         return self._deliver(self.acc.clone())
 
+    @_on_own_device
     def pop(self, on_device: bool = False) -> torch.Tensor:
         self._flush(final_W=self.cur_w if self._weighted() else None)
         out = self.acc.view(self.shape) if on_device else self._deliver(self.acc)
@@ -721,6 +743,7 @@ class _DeviceEntry(_TensorEntry):
         has been drained into the accumulator from +0 yet."""
         return self.acc is None
 
+    @_on_own_device
     def partial(self, acc_in: Optional[torch.Tensor], W=None) -> torch.Tensor:
         """This key's rows reduced in arrival order ONTO ``acc_in`` (None:
         from +0), divided by fl32(W) when W is given; releases the rows.  The
@@ -739,6 +762,7 @@ class _DeviceEntry(_TensorEntry):
         self.acc = None
         return out
 
+    @_on_own_device
     def pop_step(self, step: ops.ServerStep) -> None:
         """pop(on_device=True) followed by step.apply(avg), fused into the last
         drain when rows are pending, the step's operands allow it and the
@@ -888,6 +912,7 @@ class _RefDeviceEntry(_TensorEntry):
                 and value.device == self.dev and tuple(value.shape) == self.shape
                 and not value.requires_grad and _ref_weight(weight))
 
+    @_on_own_device
     def add(self, value: torch.Tensor, weight) -> None:
         new_w = self.cur_w + weight  # TypeError for weight=None, as the reference
         src = value.detach() if value.requires_grad else value
@@ -925,20 +950,24 @@ class _RefDeviceEntry(_TensorEntry):
     def _weighted(self) -> bool:
         return not (self.cur_w is None or self.cur_w == 0)
 
+    @_on_own_device
     def get_sum(self) -> torch.Tensor:
         self._drain()
         return self.acc.view(self.shape).clone()
 
+    @_on_own_device
     def get(self) -> torch.Tensor:
         s = self.get_sum()
         return reference_quotient(s, self.cur_w) if self._weighted() else s
 
+    @_on_own_device
     def pop(self, on_device: bool = False) -> torch.Tensor:
         self._drain()
         s = self.acc.view(self.shape)
         self.acc = None
         return reference_quotient(s, self.cur_w) if self._weighted() else s
 
+    @_on_own_device
     def pop_step(self, step: ops.ServerStep) -> None:
         step.apply(self.pop().reshape(-1).to(step.cloud.device, torch.float32).contiguous())
 
