@@ -29,7 +29,6 @@ aggregation itself is still the HIP kernel).
 """
 from __future__ import annotations
 
-import sys
 from typing import Optional
 
 import torch
@@ -80,47 +79,21 @@ def serial_aggregation(
     return True
 
 
-def _refcount(t) -> int:
-    return sys.getrefcount(t)
-
-
-def _count_in_callee(t) -> int:
-    return _refcount(t)
-
-
-def _owned_refs() -> int:
-    """References to a tensor held only by a message dict and one local
-    variable, seen from a function it is passed to, as serial_aggregation
-    passes ``params`` to _handed_over (measured, not assumed: CPython's count
-    includes the calls' own argument references)."""
-    msg = {"local_params": torch.empty(1)}
-    params = msg["local_params"]
-    return _count_in_callee(params)
-
-
-_OWNED_REFS = _owned_refs()
-
-
 def _handed_over(t: torch.Tensor) -> bool:
     """Whether ``t`` was given away by its client, so the aggregator may read
-    it after add returns.  Inside the round driver: an explicit hand-over
-    token (utils/handover.py) and no alias of its storage -- no reference
-    counting.  Outside it (receive_from_client called by user code): the
-    secondary guard, the message holding the only reference to ``t``
-    (calibrated reference count, _owned_refs) and no alias.  Called with
-    serial_aggregation's ``params`` local, as _owned_refs measures."""
+    it after add returns: an explicit hand-over token of the open
+    ``handover_round`` (utils/handover.py) and no alias of its storage.
+    Ownership is never inferred: outside a hand-over round (user code calling
+    receive_from_client on its own) no vector is handed over, and a borrowing
+    aggregator gets the reference's clone -- user code that wants the borrow
+    opens ``handover_round()`` and calls ``hand_over`` as the driver does."""
     if isinstance(t, SlabRow) and t.in_slab and not t._committed:
         # a row the client reserved in the round's slab (reserve_round_row):
         # handed over by that protocol -- it is the aggregator's own memory,
         # and torch ops on the SlabRow afterwards act on a private copy
         take_token(t)
         return True
-    token = take_token(t)
-    if token is not None:
-        return token and unaliased(t)
-    if not isinstance(t, torch.Tensor) or _refcount(t) > _OWNED_REFS:
-        return False
-    return unaliased(t)
+    return bool(take_token(t)) and unaliased(t)
 
 
 def _would_borrow(aggregator, t) -> bool:

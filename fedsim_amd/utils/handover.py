@@ -29,8 +29,10 @@ A producer that calls ``hand_over`` and still changes the very tensor in
 place before the round is reduced breaks its declaration: the version
 counter makes that reduction raise instead of reading changed data.
 
-Outside a driver round (``receive_from_client`` called by user code) no
-token exists and serial_aggregation falls back to a reference-count guard.
+Outside a hand-over round (``receive_from_client`` called by user code) no
+token exists: nothing is handed over and a borrowing aggregator gets the
+reference's clone.  User code that wants the borrow declares it the same way:
+``with handover_round(): ... hand_over(v) ...``.
 """
 from __future__ import annotations
 
@@ -84,9 +86,9 @@ def handover_round():
 
 
 def take_token(t) -> Optional[bool]:
-    """None outside a driver round (no decision: the caller's guard
-    applies); else whether ``t`` carries a valid token of the open round
-    (consumed) and its storage was not handed over before this round."""
+    """None outside a hand-over round (nothing was declared); else whether
+    ``t`` carries a valid token of the open round (consumed) and its storage
+    was not handed over before in this round."""
     if not _OPEN:
         return None
     rnd = _OPEN[-1]

@@ -395,21 +395,30 @@ def test_client_reusing_its_buffer_matches_reference(dev):
     np.testing.assert_array_equal(bits(got), bits(want))
     assert {k: float(v) for k, v in scores.items()} == run["scores"]
 
-    # a fresh, sole-owned vector is borrowed (no copy), a kept one is cloned
+    # outside the driver: a vector declared in the caller's own hand-over
+    # round is borrowed (no copy); an undeclared one -- even one only its
+    # message references -- and a kept one are cloned
     from fedsim_amd.distributed.centralized.training import serial_aggregation
     from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.handover import hand_over, handover_round
 
     agg = SerialAggregator(borrow=True)
+    with handover_round():
+        msg = dict(local_params=hand_over(torch.ones(4096, device=dev)),
+                   num_samples=dict(train=3), diverged=False, metrics=dict())
+        ptr = msg["local_params"].data_ptr()
+        assert serial_aggregation(None, 0, msg, "train", agg)
+    entry = agg._members["local_params"]
+    assert entry.borrowed[0][0].data_ptr() == ptr
     msg = dict(local_params=torch.ones(4096, device=dev), num_samples=dict(train=3),
                diverged=False, metrics=dict())
     ptr = msg["local_params"].data_ptr()
-    assert serial_aggregation(None, 0, msg, "train", agg)
-    entry = agg._members["local_params"]
-    assert entry.borrowed[0][0].data_ptr() == ptr
+    assert serial_aggregation(None, 1, msg, "train", agg)
+    assert entry.borrowed[1][0].data_ptr() != ptr
     kept = torch.ones(4096, device=dev)
     msg = dict(local_params=kept, num_samples=dict(train=3), diverged=False, metrics=dict())
-    assert serial_aggregation(None, 1, msg, "train", agg)
-    assert entry.borrowed[1][0].data_ptr() != kept.data_ptr()
+    assert serial_aggregation(None, 2, msg, "train", agg)
+    assert entry.borrowed[2][0].data_ptr() != kept.data_ptr()
     kept.fill_(5.0)  # the caller still owns it and may change it
     assert torch.equal(agg.pop("local_params"), torch.ones(4096, device=dev))
 
@@ -456,7 +465,6 @@ def test_driver_borrows_by_hand_over_token(keep_view, dev, monkeypatch):
     decisions = []
     real = U._handed_over
     monkeypatch.setattr(U, "_handed_over", lambda t: decisions.append(real(t)) or decisions[-1])
-    monkeypatch.setattr(U, "_refcount", lambda t: pytest.fail("reference count consulted"))
     base = S.make_algorithm(FedAvg)
     cls = type("KeepView", (base,), {"send_to_server": staticmethod(_keep_view_send)}) \
         if keep_view else base

@@ -433,18 +433,14 @@ def test_async_host_staging_threshold():
     assert 199_210 < _ASYNC_STAGE_MIN <= 1_085_668
 
 
-def test_hand_over_tokens_decide_borrowing_in_the_driver(monkeypatch):
-    """Inside a driver round, serial_aggregation's ownership test is the
-    explicit hand-over token plus the no-alias check -- the reference count
-    is never consulted; outside one, the reference-count guard applies."""
+def test_hand_over_tokens_decide_borrowing():
+    """serial_aggregation's ownership test is the explicit hand-over token
+    plus the no-alias check; outside a hand-over round nothing is handed over
+    -- not even a vector only its message references (no inference)."""
     from fedsim_amd.distributed.centralized.training import utils as U
     from fedsim_amd.utils.handover import hand_over, handover_round
 
-    def no_refcount(t):
-        raise AssertionError("the driver's borrow decision must not count references")
-
     with handover_round():
-        monkeypatch.setattr(U, "_refcount", no_refcount)
         fresh = hand_over(torch.ones(8))
         assert U._handed_over(fresh)
         assert not U._handed_over(fresh)  # a token is consumed once
@@ -462,13 +458,15 @@ def test_hand_over_tokens_decide_borrowing_in_the_driver(monkeypatch):
         assert U._handed_over(again)
         alias = hand_over(again.detach())  # the same storage a second time
         assert not U._handed_over(alias)
-        monkeypatch.undo()
-    # outside a round: hand_over is a no-op and the reference count decides
+    # outside a round hand_over is a no-op: the sole-owned vector is cloned
     msg = {"local_params": hand_over(torch.ones(8))}
     params = msg["local_params"]
-    assert U._handed_over(params)  # the message holds the only reference
-    kept = params  # noqa: F841 -- the client keeps it
     assert not U._handed_over(params)
+    assert not U._handed_over(torch.ones(8))
+    # the caller's own round declares it
+    with handover_round():
+        msg = {"local_params": hand_over(torch.ones(8))}
+        assert U._handed_over(msg["local_params"])
 
 
 def test_hand_over_round_scope_releases_tokens():

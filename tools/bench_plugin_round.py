@@ -31,6 +31,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fedsim_amd.distributed.centralized.training import FedAvg  # noqa: E402
 from fedsim_amd.utils import SerialAggregator, Storage  # noqa: E402
+from fedsim_amd.utils.handover import hand_over, handover_round  # noqa: E402
 
 CONFIGS = {
     "cfg1": (5, 199_210),
@@ -57,8 +58,9 @@ def messages(K, P, where, dev, seed=11):
 
 def one_round(msgs, cloud, borrow):
     """``msgs`` is consumed: each message is handed over as the round driver
-    hands it (the aggregator may borrow its tensor only if nothing else
-    holds it, training/utils.py _handed_over)."""
+    hands it (a ``handover_round`` with the client's ``hand_over`` of its
+    vector, utils/handover.py; the aggregator borrows it only then and only
+    if nothing else holds it, training/utils.py _handed_over)."""
     st = Storage()
     st.write("cloud_params", cloud)
     st.write("optimizer", torch.optim.SGD(params=[cloud], lr=1.0))
@@ -66,10 +68,12 @@ def one_round(msgs, cloud, borrow):
     agg = SerialAggregator(expected_rows=len(msgs), borrow=borrow)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(len(msgs)):
-        msg, msgs[k] = msgs[k], None
-        FedAvg.receive_from_client(st, k, msg, "train", agg, None)
-        del msg
+    with handover_round():
+        for k in range(len(msgs)):
+            msg, msgs[k] = msgs[k], None
+            hand_over(msg["local_params"])  # the client's send_to_server does this
+            FedAvg.receive_from_client(st, k, msg, "train", agg, None)
+            del msg
     t1 = time.perf_counter()
     FedAvg.optimize(st, agg, None)
     torch.cuda.synchronize()
@@ -143,11 +147,11 @@ def headline_round(K, P, dev, mode, reps, ragged=False):
                                slab_bytes=4 * (K + 1) * ((P + C - 1) // C) * C)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        with slab_rows.round_aggregator(agg):
+        with slab_rows.round_aggregator(agg), handover_round():
             for k in range(K):
                 row = slab_rows.reserve_round_row("local_params", model) \
                     if mode == "slab_rows" else None
-                msg = dict(local_params=vectorize_module(model, out=row), num_steps=1,
+                msg = dict(local_params=hand_over(vectorize_module(model, out=row)), num_steps=1,
                            diverged=False, num_samples={"train": w[k]},
                            metrics={"train": {"cross_entropy_score": 1.0}})
                 del row

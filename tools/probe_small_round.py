@@ -27,6 +27,7 @@ from fedsim_amd.distributed.centralized.training import FedAvg  # noqa: E402
 from fedsim_amd.distributed.centralized.training import utils as tu  # noqa: E402
 from fedsim_amd.utils import SerialAggregator, Storage  # noqa: E402
 from fedsim_amd.utils import aggregators as A  # noqa: E402
+from fedsim_amd.utils.handover import hand_over, handover_round  # noqa: E402
 
 T = collections.defaultdict(list)
 
@@ -69,10 +70,12 @@ def main():
         if rep == 3:
             T.clear()
         t0 = time.perf_counter()
-        for k in range(a.K):
-            msg, msgs[k] = msgs[k], None
-            FedAvg.receive_from_client(st, k, msg, "train", agg, None)
-            del msg
+        with handover_round():
+            for k in range(a.K):
+                msg, msgs[k] = msgs[k], None
+                hand_over(msg["local_params"])
+                FedAvg.receive_from_client(st, k, msg, "train", agg, None)
+                del msg
         t1 = time.perf_counter()
         FedAvg.optimize(st, agg, None)
         torch.cuda.synchronize()
