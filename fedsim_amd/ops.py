@@ -290,10 +290,12 @@ def reduce_blocked(
 
 def pack_row(src: torch.Tensor, Xb: torch.Tensor, r: int, stream=None) -> None:
     """Copy one client vector (contiguous fp32; pinned host or HIP memory) into
-    row ``r`` of the column-blocked slab ``Xb`` with one 2-D DMA, ordered on
-    ``stream`` (default: the current stream of Xb's device).
+    row ``r`` of the column-blocked slab ``Xb``, ordered on ``stream``
+    (default: the current stream of Xb's device): a copy kernel, reading a
+    page-locked host vector in place over PCIe, or a 2-D DMA where the source
+    is not 16-byte aligned.
 
-    The DMA is asynchronous and bypasses torch's copy bookkeeping: the caller
+    The copy is asynchronous and bypasses torch's copy bookkeeping: the caller
     keeps ``src`` alive and unmodified until ``stream`` has passed the copy
     (the aggregator's staging ring does this with per-slot events)."""
     _require_hip_f32(Xb, "Xb")

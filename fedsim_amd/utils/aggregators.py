@@ -8,9 +8,10 @@ tensor-valued keys are reduced on the MI355X by libfedagg:
   vector into a column-blocked HBM ring slab and records ``fl32(weight)``; the
   running weight is the same Python sum ``cur_w + weight`` as the reference (so
   ``weight=None`` raises the same TypeError).  HIP-resident vectors are packed
-  with a D2D 2-D DMA on the compute stream; host vectors are snapshotted into a
-  pinned staging ring and DMA'd on a separate copy stream, overlapping the
-  reductions.
+  by a copy kernel on the compute stream; host vectors are snapshotted into a
+  pinned staging ring and packed on a separate copy stream (the pack kernel
+  reading the slot in place over PCIe, or a DMA: ``_HOST_PACK``), overlapping
+  the reductions.
 * Pending rows are reduced by the exact-mode kernel into an fp32 accumulator in
   arrival order whenever the ring needs room, and at ``get`` / ``pop``
   (aggregators.py:42-60, 104-122), where the divide by ``fl32(W)`` is fused
@@ -95,6 +96,20 @@ _STAGING_SLOTS = 3
 # 43-46 for torch's copy_, whose 16 threads take the host memory bandwidth
 # the concurrent DMA reads from).  "auto" takes each below / from 32 MB.
 _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
+# How a page-locked host vector (the caller's, or the staging slot) reaches
+# its slab row: "zero_copy", the pack kernel reading it in place over PCIe
+# (fedagg_pack_row_f32 on a mapped host pointer: no DMA to issue), "dma", a
+# DMA into a device slot and then the HBM pack (rounds 1-5), or "auto".
+# Interleaved on one box (tools/ab_host_pack.py, profiles/r06w/, r06x/): for
+# vectors staged from pageable memory the kernel wins below 64 MB (config 1
+# rounds 0.45 vs 0.52 ms, config 2 K=1000 113 vs 124 ms, 4.3 / 32 MB
+# host->host rounds 36.1 / 48.4 vs 34.3 / 44.4 GB/s) and the two are within
+# noise at 100 MB; for the caller's own pinned vectors, whose put waits for
+# the copy, the DMA engine wins (4.3 / 32 / 100 MB: 36.3 / 51.2 / 52.5 vs
+# 31.9 / 47.7 / 50.9 GB/s).  "auto" takes the kernel for staged vectors
+# below 64 MB and the DMA otherwise.
+_HOST_PACK = os.environ.get("FEDSIM_AMD_HOST_PACK", "auto")
+_ZERO_COPY_MAX = 64 << 20
 _STAGE_SPLIT_MIN = 32 << 20
 _stage_pool: Optional[ThreadPoolExecutor] = None
 
@@ -256,7 +271,6 @@ class _Ingest(object):
         if self.events[i] is not None:
             self.events[i].synchronize()
         P = src.numel()
-        dslot = self._slot(self.dbufs, i, P, device=self.dev)
         if src.is_pinned():
             host = src  # DMA straight from the caller's pinned buffer
         else:
@@ -268,11 +282,16 @@ class _Ingest(object):
             # microseconds per client
             _staging_copy(host, src)
             self._check_version(src, version)  # not changed while it was copied
-        with torch.cuda.stream(self.stream):
-            dslot.copy_(host, non_blocking=True)
+        packed = host  # the pack kernel reads it in place over PCIe
+        if _HOST_PACK == "dma" or (_HOST_PACK == "auto" and (
+                host is src or 4 * P >= _ZERO_COPY_MAX)):
+            # a DMA into a device slot, then the HBM pack
+            packed = self._slot(self.dbufs, i, P, device=self.dev)
+            with torch.cuda.stream(self.stream):
+                packed.copy_(host, non_blocking=True)
         if wait_event is not None:
             self.stream.wait_event(wait_event)
-        ops.pack_row(dslot, Xb, r, stream=self.stream)
+        ops.pack_row(packed, Xb, r, stream=self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)
         self.events[i] = ev

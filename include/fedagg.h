@@ -334,7 +334,9 @@ int fedagg_unpack_row_f32(const float* Xb, int64_t Kcap, int64_t C, int64_t r, i
 
 /*
  * Pack one client vector (P contiguous fp32, host-pinned or device memory)
- * into row r of a column-blocked slab [ceil(P/C), Kcap, C] with one 2-D DMA.
+ * into row r of a column-blocked slab [ceil(P/C), Kcap, C]: a copy kernel
+ * for 16-byte aligned device memory and for page-locked host memory mapped
+ * at its own address (read in place over PCIe), else one 2-D DMA.
  * This is the HBM side of SerialAggregator.add's snapshot (the reference's
  * clone at fedsim/distributed/centralized/training/utils.py:34) and of
  * vectorize_module's packing (fedsim/utils/convert_parameters.py:78-94).

@@ -483,6 +483,38 @@ def test_driver_borrows_by_hand_over_token(keep_view, dev, monkeypatch):
     assert all(decisions) if not keep_view else not any(decisions)
 
 
+@pytest.mark.parametrize("mode", ["auto", "zero_copy", "dma"])
+@pytest.mark.parametrize("borrow_host", [False, True])
+def test_host_pack_modes_are_exact(dev, mode, borrow_host, monkeypatch):
+    """Host vectors reach their slab rows either through the pack kernel
+    reading the page-locked slot (or the caller's pinned tensor) in place over
+    PCIe, or through a DMA into a device slot (aggregators._HOST_PACK): every
+    mode gives the oracle's round bit for bit -- pageable and pinned sources,
+    a pinned source at an offset that is not 16-byte aligned (the 2-D DMA),
+    tails that are not a multiple of 4, and more rows than staging slots."""
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils import aggregators as A
+
+    monkeypatch.setattr(A, "_HOST_PACK", mode)
+    for K, P in ((7, 4099), (5, 199_210), (4, A._ASYNC_STAGE_MIN + 5)):
+        X = V.client_rows("realistic", K, P, 12)
+        w = V.client_weights("fedavg", K, 12)
+        agg = SerialAggregator(borrow=True, borrow_host=borrow_host, max_rows=3)
+        pin_base = torch.empty(P + 1).pin_memory()
+        for k in range(K):
+            src = torch.from_numpy(X[k].copy())
+            if k % 3 == 1:
+                src = src.pin_memory()
+            elif k % 3 == 2:  # pinned, 4 bytes off a 16-byte boundary
+                src = pin_base[1:]
+                src.copy_(torch.from_numpy(X[k]))
+            agg.add("p", src, w[k])
+            if k % 3 == 2:
+                agg.get_sum("p")  # the shared pinned buffer is read before reuse
+        np.testing.assert_array_equal(bits(agg.pop("p").numpy()),
+                                      bits(ref.reduce(X, w, W=sum(w))))
+
+
 def test_handed_over_host_rows_are_staged_after_add(dev):
     """borrow_host=True with host vectors (the round driver's aggregator under
     device="cpu"): each handed-over vector is copied into pinned staging and
