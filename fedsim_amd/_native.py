@@ -23,11 +23,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, _LIB_NAME))
 
 # Must match include/fedagg.h
-ABI_VERSION = 5  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
+ABI_VERSION = 6  # 2: round-2 entry points (teacher / pool / pack_segments / unpack_row);
 #                 3: the rejected flat-load / LDS-weight flag bits refused;
 #                 4: + fedagg_finalize_f64, fedagg_reduce_rows_ref (fp64 / bf16 /
 #                    fp16 keys of the generic aggregator);
-#                 5: + fedagg_rows_plan (which kernel a borrowed-rows call takes)
+#                 5: + fedagg_rows_plan (which kernel a borrowed-rows call takes);
+#                 6: + fedagg_host_mapped (page-locked host operands in place)
 FEDAGG_INIT = 0x1
 FEDAGG_FINALIZE = 0x2
 FEDAGG_NT = 0x4
@@ -147,6 +148,7 @@ SIGNATURES = {
         [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
          ctypes.c_int64, ctypes.c_void_p],
     ),
+    "fedagg_host_mapped": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "fedagg_pack_segments_f32": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,

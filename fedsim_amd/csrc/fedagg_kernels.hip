@@ -3909,6 +3909,31 @@ int fedagg_pad_lrn_maxpool_f32(const float* x, const fedagg_pool_args* args, flo
   return static_cast<int>(hipGetLastError());
 }
 
+// Page-locked host memory (hipHostMalloc: torch's pin_memory) that the GPU
+// reaches at the host address itself: kernels read and write it in place over
+// PCIe -- 46-56 GB/s from 0.8 MB on, with no DMA to issue
+// (tools/zero_copy_probe.hip, profiles/r06v/).
+static bool host_mapped_here(const void* q) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not registered with HIP
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost) return false;
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, const_cast<void*>(q), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return dp == q;
+}
+
+int fedagg_host_mapped(const void* p, int64_t nbytes) {
+  if (!p || nbytes < 0) return FEDAGG_EINVAL;
+  const char* c = static_cast<const char*>(p);
+  return host_mapped_here(c) && (nbytes == 0 || host_mapped_here(c + nbytes - 1)) ? 1 : 0;
+}
+
 int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, int64_t C,
                         int64_t r, void* stream) {
   if (P < 0 || Kcap <= 0 || r < 0 || r >= Kcap) return FEDAGG_EINVAL;
@@ -3918,25 +3943,20 @@ int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, in
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipPointerAttribute_t attr;
   const bool known = hipPointerGetAttributes(&attr, src) == hipSuccess;
+  (void)hipGetLastError();  // clear a failed query on pageable memory
+  // HBM -> HBM, or page-locked host memory read in place over PCIe: the copy
+  // kernel on the CUs; anything else (pageable, or mapped elsewhere) the DMA
   const float* from = nullptr;
-  if (known && attr.type == hipMemoryTypeDevice) {
-    from = src;  // HBM -> HBM: copy kernel on the CUs
-  } else if (known && attr.type == hipMemoryTypeHost) {
-    // page-locked host memory (hipHostMalloc: mapped into the GPU's address
-    // space): the same kernel reads it in place over PCIe -- 46-56 GB/s from
-    // 0.8 MB on, with no DMA to issue (tools/zero_copy_probe.hip,
-    // profiles/r06v/).  Only where the mapping is the host address itself,
-    // as hipHostMalloc gives on this platform; anything else takes the DMA.
-    void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, const_cast<float*>(src), 0) == hipSuccess && dp == src)
-      from = src;
-  }
+  if (known && attr.type == hipMemoryTypeDevice)
+    from = src;
+  else if (known && attr.type == hipMemoryTypeHost &&
+           fedagg_host_mapped(src, 4 * P) == 1)
+    from = src;
   if (from && aligned16(from) && aligned16(Xb)) {
     hipLaunchKernelGGL(k_pack_row, dim3(pack_grid(P)), dim3(kBlock), 0, s, from,
                        P, Xb, Kcap, C, r);
     return static_cast<int>(hipGetLastError());
   }
-  (void)hipGetLastError();  // clear a failed query on pageable memory
   const int64_t full = P / C;
   const int64_t rem = P - full * C;
   float* dst = Xb + r * C;

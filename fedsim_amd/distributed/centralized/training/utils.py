@@ -29,6 +29,7 @@ aggregation itself is still the HIP kernel).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -227,23 +228,52 @@ def _host_state(cloud, aux, prev, dev) -> bool:
                for t in (aux, prev))
 
 
+# How host-resident server state reaches the step kernel: "zero_copy", the
+# kernel reading and writing one page-locked buffer in place over PCIe (no
+# DMA to issue either way), or "dma", one pinned DMA each way (round 5).
+_HOST_STEP = os.environ.get("FEDSIM_AMD_HOST_STEP", "zero_copy")
+
+
 def _fused_server_step_host(algo, cloud, avg, source, optimizer, cfg, coef, aux, want_avg_prev,
                             dev, prev):
-    """fused_server_step for host-resident server state: the state crosses
-    PCIe as ONE pinned DMA each way instead of one pageable copy per tensor
-    (H2D of the cloud, D2H of the cloud and of its grad, plus the momentum
-    buffer / aux / previous average when the algorithm has them).  One device
-    buffer holds every vector the kernel reads or writes; the results come
-    back into one pinned buffer whose rows become ``cloud.grad``, the
-    momentum buffer and the returned vectors (fresh tensors each round, as
-    the reference's step leaves them).  Same kernel, same bits."""
+    """fused_server_step for host-resident server state (FedSim's
+    device="cpu" runs): the cloud -- and the aux vector, momentum buffer and
+    previous average when the algorithm has them -- are copied into ONE
+    page-locked buffer whose rows the step kernel reads and writes in place
+    over PCIe (ops.host_mapped), instead of a pageable copy per tensor each
+    way; its rows become ``cloud.grad``, the momentum buffer and the returned
+    vectors (fresh tensors each round, as the reference's step leaves them).
+    With ``_HOST_STEP = "dma"``, or a sharded aggregator (whose collectives
+    need the operands in HBM), the buffer crosses PCIe as one pinned DMA each
+    way instead.  Same kernel, same bits."""
     P = cloud.numel()
     rows = ["c", "g"] + (["x"] if aux is not None else []) + \
         (["ap"] if want_avg_prev else []) + (["buf"] if cfg["momentum"] != 0 else [])
     at = {name: i for i, name in enumerate(rows)}
-    D = torch.empty(len(rows), P, dtype=torch.float32, device=dev)
     ins = [("c", cloud.data)] + ([("x", aux)] if aux is not None else []) + \
         ([("buf", prev)] if prev is not None else [])
+    if _HOST_STEP == "zero_copy" and (source is None or
+                                      type(source[0]) is _DeviceSerialAggregator):
+        # rows padded to 16 bytes: the fused reduce + step entries take them
+        H = torch.empty(len(rows), -(-P // 4) * 4, dtype=torch.float32, pin_memory=True)
+        if ops.host_mapped(H):
+            row = {name: H[i, :P] for i, name in enumerate(rows)}
+            for name, t in ins:
+                row[name].copy_(t.detach().reshape(-1))
+            step = ops.ServerStep(
+                algo, row["c"], lr=cfg["lr"], momentum=cfg["momentum"],
+                dampening=cfg["dampening"], weight_decay=cfg["weight_decay"],
+                nesterov=cfg["nesterov"], maximize=cfg["maximize"], coef=coef,
+                aux=row.get("x"), avg_prev=row.get("ap"), momentum_buf=row.get("buf"),
+                momentum_init=cfg["momentum"] != 0 and prev is None, grad_out=row["g"],
+                device=dev)
+            if source is not None:
+                source[0].pop_step(source[1], step)
+            else:
+                step.apply((avg if avg.device == dev else avg.to(dev)).reshape(-1).contiguous())
+            torch.cuda.current_stream(dev).synchronize()
+            return _host_step_results(cloud, optimizer, aux, want_avg_prev, row)
+    D = torch.empty(len(rows), P, dtype=torch.float32, device=dev)
     hin = torch.empty(len(ins), P, dtype=torch.float32, pin_memory=True)
     for j, (name, t) in enumerate(ins):
         hin[j].copy_(t.detach().reshape(-1))
@@ -270,7 +300,12 @@ def _fused_server_step_host(algo, cloud, avg, source, optimizer, cfg, coef, aux,
     done = torch.cuda.Event()
     done.record(cur)
     done.synchronize()
-    out = {name: hout[i] for i, name in enumerate(rows)}
+    return _host_step_results(cloud, optimizer, aux, want_avg_prev,
+                              {name: hout[i] for i, name in enumerate(rows)})
+
+
+def _host_step_results(cloud, optimizer, aux, want_avg_prev, out):
+    """The host step's rows handed back as optimizer.step() leaves them."""
     cloud.data.copy_(out["c"].view_as(cloud))
     optimizer.zero_grad()
     cloud.grad = out["g"].view_as(cloud)

@@ -690,6 +690,23 @@ def feddyn_sgd(avg: torch.Tensor, cloud: torch.Tensor, h: torch.Tensor, ratio: f
     return cloud
 
 
+def host_mapped(t: torch.Tensor) -> bool:
+    """Whether ``t`` is page-locked host memory the GPU reaches at its own
+    address (fedagg_host_mapped: torch's pin_memory on this platform), so a
+    kernel can read and write it in place over PCIe."""
+    if not isinstance(t, torch.Tensor) or t.device.type != "cpu" or not t.is_pinned():
+        return False
+    nbytes = t.numel() * t.element_size()
+    return nbytes == 0 or _native.load().fedagg_host_mapped(t.data_ptr(), nbytes) == 1
+
+
+def _require_hip_step(step: "ServerStep") -> None:
+    """A kernel is launched on the step: it runs on a HIP device (its
+    operands there or host-mapped, checked at construction)."""
+    if step.device.type != "cuda":
+        raise ValueError(f"cloud must live on a HIP device, got {step.device}")
+
+
 ALGO = {"fedavg": _native.FEDAGG_ALGO_FEDAVG, "adabest": _native.FEDAGG_ALGO_ADABEST,
         "feddyn": _native.FEDAGG_ALGO_FEDDYN}
 
@@ -711,11 +728,16 @@ class ServerStep(object):
                  aux: Optional[torch.Tensor] = None, avg_prev: Optional[torch.Tensor] = None,
                  momentum_buf: Optional[torch.Tensor] = None, momentum_init: bool = False,
                  grad_out: Optional[torch.Tensor] = None,
-                 avg_out: Optional[torch.Tensor] = None) -> None:
+                 avg_out: Optional[torch.Tensor] = None,
+                 device: Optional[torch.device] = None) -> None:
         if algo not in ALGO:
             raise ValueError(f"unknown algo {algo!r}")
         self.P = P = cloud.numel()
         self.cloud = cloud
+        # the GPU the step runs on: every operand lives there, or is
+        # page-locked host memory the kernel reads and writes in place over
+        # PCIe (host_mapped: FedSim's device="cpu" server state)
+        self.device = cloud.device if device is None else torch.device(device)
         operands = ((cloud, "cloud"), (aux, "aux"), (avg_prev, "avg_prev"),
                     (momentum_buf, "momentum_buf"), (grad_out, "grad_out"), (avg_out, "avg_out"))
         for t, n in operands:
@@ -727,8 +749,9 @@ class ServerStep(object):
                     raise TypeError(f"{n} must be a float32 tensor")
                 if t.numel() != P or not t.is_contiguous():
                     raise ValueError(f"{n} must be contiguous with {P} elements")
-                if t.device != cloud.device:
-                    raise ValueError(f"{n} is on {t.device}, cloud on {cloud.device}")
+                if t.device != self.device and not (
+                        self.device.type == "cuda" and host_mapped(t)):
+                    raise ValueError(f"{n} is on {t.device}, the step runs on {self.device}")
         self.algo = algo
         self.operands = {n: t for t, n in operands if t is not None}
         self._scalars = dict(lr=lr, momentum=momentum, dampening=dampening,
@@ -752,7 +775,7 @@ class ServerStep(object):
         operand): what one rank of a parameter-sharded round runs."""
         views = {n: t[lo:hi] for n, t in self.operands.items()}
         cloud = views.pop("cloud")
-        return ServerStep(self.algo, cloud, **self._scalars, **views)
+        return ServerStep(self.algo, cloud, **self._scalars, **views, device=self.device)
 
     def outputs(self):
         """The operands the step writes (cloud and whichever of aux /
@@ -761,16 +784,16 @@ class ServerStep(object):
 
     def apply(self, avg: torch.Tensor) -> torch.Tensor:
         _require_hip_f32(avg, "avg")
-        _require_hip_f32(self.cloud, "cloud")
+        _require_hip_step(self)
         if avg.numel() != self.P or not avg.is_contiguous():
             raise ValueError(f"avg must be contiguous with {self.P} elements")
-        if avg.device != self.cloud.device:
-            raise ValueError(f"avg is on {avg.device}, cloud on {self.cloud.device}")
+        if avg.device != self.device:
+            raise ValueError(f"avg is on {avg.device}, the step runs on {self.device}")
         a = self.args
         rc = _native.load().fedagg_server_step_f32(
             a.algo, avg.data_ptr(), a.coef, a.cloud, a.aux, a.avg_prev, a.momentum_buf,
             a.momentum_init, a.grad_out, ctypes.byref(self.sgd), self.P,
-            _stream_ptr(self.cloud.device),
+            _stream_ptr(self.device),
         )
         check(rc, "fedagg_server_step_f32")
         avg_out = self.operands.get("avg_out")
@@ -790,7 +813,7 @@ def can_fuse_step(Xb: torch.Tensor, step: ServerStep) -> bool:
     """Whether fedagg_reduce_step_blocked_f32 accepts this slab and step."""
     return (Xb.dim() == 3 and Xb.shape[2] in BLOCK_COLS
             and Xb.shape[1] * Xb.shape[2] * 4 < (1 << 32) and step.aligned()
-            and Xb.device == step.cloud.device)
+            and Xb.device == step.device)
 
 
 # Below 2^24 columns the narrow kernels' grid is a few generations of resident
@@ -838,9 +861,9 @@ def reduce_blocked_step(
     _require_hip_f32(w32, "w32")
     if Xb.dim() != 3 or not Xb.is_contiguous():
         raise ValueError("Xb must be a contiguous [nblk, Kcap, C] tensor")
-    if step.cloud.device != Xb.device:
-        raise ValueError(f"the step's operands are on {step.cloud.device}, the slab on "
-                         f"{Xb.device}")
+    _require_hip_step(step)
+    if step.device != Xb.device:
+        raise ValueError(f"the step runs on {step.device}, the slab is on {Xb.device}")
     nb, Kcap, C = Xb.shape
     P = step.P
     if nb != (P + C - 1) // C:
@@ -901,15 +924,15 @@ def reduce_rows_step(
     validated every row (the aggregator does at ``add``), skip the per-row
     checks."""
     _require_hip_f32(w32, "w32")
-    _require_hip_f32(step.cloud, "cloud")
-    P, dev = step.P, step.cloud.device
+    _require_hip_step(step)
+    P, dev = step.P, step.device
     B = len(rows)
     for i, r in enumerate(() if checked else rows):
         _require_hip_f32(r, f"rows[{i}]")
         if r.numel() != P or not r.is_contiguous() or r.data_ptr() % 16:
             raise ValueError(f"rows[{i}] must be contiguous, 16-B aligned, {P} elements")
         if r.device != dev:
-            raise ValueError(f"rows[{i}] is on {r.device}, cloud on {dev}")
+            raise ValueError(f"rows[{i}] is on {r.device}, the step runs on {dev}")
     if w32.numel() < B:
         raise ValueError("w32 too short")
     if not step.aligned():

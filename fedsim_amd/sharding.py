@@ -360,7 +360,7 @@ class _DevicesEntry(_TensorEntry):
         """Each GPU runs the step on its slice: in place when the operands
         live on that GPU, else on a copy of the operand slices moved over
         that GPU's own link (PCIe for a host-resident cloud), copied back."""
-        home = step.cloud.device
+        home = step.device
         back = []
         for (lo, hi), inner in zip(self.spans, self.inners):
             if inner is None:
@@ -823,7 +823,7 @@ class _ClientShardRef(_TensorEntry):
 
     def pop_step(self, step: ops.ServerStep) -> None:
         avg = self.get()
-        self.agg._apply_step(step, avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+        self.agg._apply_step(step, avg.reshape(-1).to(step.device, torch.float32).contiguous())
 
 
 class ClientShardedSerialAggregator(SerialAggregator):
@@ -1060,7 +1060,7 @@ class ClientShardedSerialAggregator(SerialAggregator):
         if self._step_impl is not None:
             self._step_impl(step, avg)
         else:
-            step.apply(avg if avg.device == step.cloud.device else avg.to(step.cloud.device))
+            step.apply(avg if avg.device == step.device else avg.to(step.device))
 
     def add(self, key, value, weight=None):
         """Every rank makes the same choice (the values' dtypes and shapes

@@ -787,7 +787,7 @@ class _DeviceEntry(_TensorEntry):
         drain when rows are pending, the step's operands allow it and the
         fused pass is the faster one at this size (ops.fuse_step_pays)."""
         if self.borrowed:
-            fusable = step.aligned() and step.cloud.device == self.dev
+            fusable = step.aligned() and step.device == self.dev
             rows = len(self.borrowed)
         else:
             fusable = self.n_pending > 0 and ops.can_fuse_step(self.slab, step)
@@ -988,7 +988,7 @@ class _RefDeviceEntry(_TensorEntry):
 
     @_on_own_device
     def pop_step(self, step: ops.ServerStep) -> None:
-        step.apply(self.pop().reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+        step.apply(self.pop().reshape(-1).to(step.device, torch.float32).contiguous())
 
 
 def _drop_entry(entry) -> None:
@@ -1191,11 +1191,11 @@ class SerialAggregator(object):
         e = self._entry(key)
         if not isinstance(e, _TensorEntry):
             avg = self.pop(key)
-            step.apply(avg.reshape(-1).to(step.cloud.device, torch.float32).contiguous())
+            step.apply(avg.reshape(-1).to(step.device, torch.float32).contiguous())
             return
         del self._members[key]
-        if e.dev != step.cloud.device:
-            step.apply(e.pop(on_device=True).reshape(-1).to(step.cloud.device))
+        if e.dev != step.device:
+            step.apply(e.pop(on_device=True).reshape(-1).to(step.device))
             return
         e.pop_step(step)
 

@@ -65,8 +65,9 @@ extern "C" {
    flat-load and LDS-weight A/B switches, measured and rejected) are no
    longer accepted (FEDAGG_EINVAL); 4: + fedagg_finalize_f64 and
    fedagg_reduce_rows_ref (the dtype-generic SerialAggregator's fp64 / bf16 /
-   fp16 keys); 5: + fedagg_rows_plan */
-#define FEDAGG_ABI_VERSION 5
+   fp16 keys); 5: + fedagg_rows_plan; 6: + fedagg_host_mapped (page-locked
+   host operands read and written in place) */
+#define FEDAGG_ABI_VERSION 6
 
 /* flags for the reduce entry points */
 #define FEDAGG_INIT      0x1  /* ignore acc_in: start from +0.0f (first batch of a round) */
@@ -343,6 +344,17 @@ int fedagg_unpack_row_f32(const float* Xb, int64_t Kcap, int64_t C, int64_t r, i
  */
 int fedagg_pack_row_f32(const float* src, int64_t P, float* Xb, int64_t Kcap, int64_t C,
                         int64_t r, void* stream);
+
+/*
+ * 1 if [p, p + nbytes) is page-locked host memory the GPU reaches at the
+ * host address itself (hipHostMalloc on this platform: torch's pin_memory),
+ * else 0 (pageable or device memory, or mapped at another address).  Such
+ * memory may stand in for device memory as a pack source and as a server
+ * step's operands (struct fedagg_step_args, fedagg_server_step_f32): the
+ * kernels then read and write it in place over PCIe, with no DMA to issue --
+ * the host-resident server state of FedSim's device="cpu" runs.
+ */
+int fedagg_host_mapped(const void* p, int64_t nbytes);
 
 /* out[p] = fl32(acc[p] / W32)  (IEEE true division; out may alias acc). */
 int fedagg_finalize_f32(const float* acc, float W32, int64_t P, float* out,

@@ -41,7 +41,7 @@ def test_header_declares_the_abi():
     fns = header_functions()
     assert fns == sorted([
         "fedagg_abi_version", "fedagg_strerror", "fedagg_column_mapping", "fedagg_reduce_f32",
-        "fedagg_reduce_rows_f32", "fedagg_rows_plan",
+        "fedagg_reduce_rows_f32", "fedagg_rows_plan", "fedagg_host_mapped",
         "fedagg_reduce_blocked_f32", "fedagg_pack_row_f32", "fedagg_pack_segments_f32",
         "fedagg_unpack_row_f32", "fedagg_teacher_linear_f32", "fedagg_teacher_conv2d_f32",
         "fedagg_conv_stage", "fedagg_conv_order", "fedagg_conv_pool_fusable", "fedagg_pool_output",
