@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from bench_plugin_round import messages, one_round  # noqa: E402
 
 from fedsim_amd.utils import SerialAggregator  # noqa: E402
+from fedsim_amd.distributed.centralized.training import utils as U  # noqa: E402
 from fedsim_amd.utils import aggregators as A  # noqa: E402
 
 MODES = ("dma", "zero_copy")
@@ -48,6 +49,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--h2d-only", action="store_true")
+    ap.add_argument("--step-ab", action="store_true",
+                    help="A/B the host server step (training/utils._HOST_STEP) instead, "
+                         "on the cloud-on-host rounds")
     ap.add_argument("--h2d-P", default="25000000", help="vector sizes, separated by :")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -57,21 +61,28 @@ def main():
              ("cfg2_K10_cpu_run", 10, 1_085_668, "cpu_run", 20),
              ("cfg2_K10_host_pinned", 10, 1_085_668, "host_pinned", 20),
              ("cfg2_K1000_host_pageable", 1000, 1_085_668, "host_pageable", 2)]
+    if a.step_ab:
+        cases = [c for c in cases if c[3] == "cpu_run"]
     for name, K, P, where, n in ([] if a.h2d_only else cases):
         times = {m: [] for m in MODES}
         outs = {}
         for rep in range(n + 1):
             for m in MODES:
-                A._HOST_PACK = m
+                if a.step_ab:
+                    U._HOST_STEP = m
+                else:
+                    A._HOST_PACK = m
                 t, c = plugin_round(K, P, where, dev)
                 if rep:
                     times[m].append(t)
                 outs[m] = c
         same = torch.equal(outs["dma"].view(torch.int32), outs["zero_copy"].view(torch.int32))
         res[name] = {m: round(statistics.median(v) * 1e3, 3) for m, v in times.items()}
-        res[name].update(unit="ms per round", bitwise_equal=same)
+        res[name].update(unit="ms per round", bitwise_equal=same,
+                         toggled="_HOST_STEP" if a.step_ab else "_HOST_PACK")
         print(json.dumps({name: res[name]}), flush=True)
-    for P, pinned in [(int(p), pin) for p in a.h2d_P.split(":") for pin in (True, False)]:
+    for P, pinned in [(int(p), pin) for p in a.h2d_P.split(":") for pin in (True, False)
+                      if not a.step_ab]:
         K = max(64, min(1000, int(64 * 25_000_000 // P)))  # >= 6.4 GB per round
         w = [50 + (37 * k) % 551 for k in range(K)]
         pool = [torch.empty(P).normal_() for _ in range(8)]
@@ -92,7 +103,7 @@ def main():
         res[name].update(unit="GB/s", bitwise_equal=same)
         print(json.dumps({name: res[name]}), flush=True)
         del pool, outs
-    A._HOST_PACK = "auto"
+    A._HOST_PACK, U._HOST_STEP = "auto", "zero_copy"
     print(json.dumps({"all": res}), flush=True)
 
 

@@ -44,6 +44,16 @@ def main():
     res["current_device_us"] = per_call(torch.cuda.current_device, 20000)
     res["_cuda_getDevice_us"] = per_call(torch._C._cuda_getDevice, 20000)
     res["unaliased_us"] = per_call(lambda: unaliased(t), 20000)
+    from fedsim_amd import ops
+
+    h = torch.empty(2, a.P).pin_memory()
+    res["host_mapped_us"] = per_call(lambda: ops.host_mapped(h), 5000)
+    dd = torch.empty(2, a.P, device=dev)
+    res["server_step_device_us"] = per_call(
+        lambda: ops.ServerStep("fedavg", dd[0], lr=1.0, grad_out=dd[1]), 5000)
+    res["server_step_mapped_us"] = per_call(
+        lambda: ops.ServerStep("fedavg", h[0], lr=1.0, grad_out=h[1], device=dev), 5000)
+    res["pinned_alloc_us"] = per_call(lambda: torch.empty(2, a.P, pin_memory=True), 2000)
 
     def tok():
         hand_over(t)
