@@ -407,6 +407,24 @@ def test_changed_client_storage_keys():
     assert _removed_keys(st, state) == ["same"]
 
 
+def test_server_step_device_rule():
+    """A ServerStep runs on one device: its operands live there, or are
+    page-locked host memory the GPU reaches at its own address
+    (ops.host_mapped, checked on the GPU box by test_gpu_host_mapped.py);
+    pageable host operands of a HIP step are refused, and a narrowed step
+    keeps the device."""
+    from fedsim_amd import ops
+
+    assert not ops.host_mapped(torch.zeros(4)) and not ops.host_mapped(torch.zeros(0))
+    assert not ops.host_mapped("not a tensor")
+    with pytest.raises(ValueError, match="the step runs on cuda:0"):
+        ops.ServerStep("fedavg", torch.zeros(8), lr=1.0, device="cuda:0")
+    s = ops.ServerStep("fedavg", torch.zeros(8), lr=1.0, grad_out=torch.zeros(8))
+    assert s.device == torch.device("cpu") and s.narrow(2, 6).device == s.device
+    with pytest.raises(ValueError, match="HIP device"):
+        s.apply(torch.zeros(8))
+
+
 def test_host_state_step_selection():
     """fused_server_step takes the one-DMA-each-way host path exactly when
     the cloud (and the aux vector / momentum buffer it has) live in host
