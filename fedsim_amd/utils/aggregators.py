@@ -100,7 +100,7 @@ _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
 # its slab row: "zero_copy", the pack kernel reading it in place over PCIe
 # (fedagg_pack_row_f32 on a mapped host pointer: no DMA to issue), "dma", a
 # DMA into a device slot and then the HBM pack (rounds 1-5), or "auto".
-# Interleaved on one box (tools/ab_host_pack.py, profiles/r06w/, r06x/): for
+# Interleaved on one box (tools/ab_host_pack.py, profiles/r06w/): for
 # vectors staged from pageable memory the kernel wins below 64 MB (config 1
 # rounds 0.45 vs 0.52 ms, config 2 K=1000 113 vs 124 ms, 4.3 / 32 MB
 # host->host rounds 36.1 / 48.4 vs 34.3 / 44.4 GB/s) and the two are within
