@@ -259,7 +259,14 @@ def _fused_server_step_host(algo, cloud, avg, source, optimizer, cfg, coef, aux,
         if ops.host_mapped(H):
             row = {name: H[i, :P] for i, name in enumerate(rows)}
             for name, t in ins:
-                row[name].copy_(t.detach().reshape(-1))
+                t = t.detach().reshape(-1)
+                if name in ("c", "buf") and t.data_ptr() % 16 == 0 and ops.host_mapped(t):
+                    # page-locked already (init_cloud pins the cloud; the
+                    # momentum buffer is last round's row): updated in place,
+                    # as optimizer.step() updates the parameter and its buffer
+                    row[name] = t
+                else:
+                    row[name].copy_(t)
             step = ops.ServerStep(
                 algo, row["c"], lr=cfg["lr"], momentum=cfg["momentum"],
                 dampening=cfg["dampening"], weight_decay=cfg["weight_decay"],
@@ -328,6 +335,10 @@ def init_cloud(server_storage):
     server optimizer / LR scheduler over ``[cloud_params]``."""
     model = server_storage.read("model_def")().to(server_storage.read("device"))
     cloud = vectorize_module(model, clone=True, detach=True)
+    if cloud.device.type == "cpu" and torch.cuda.is_available():
+        # device="cpu" with the aggregation on the GPU: a page-locked cloud
+        # is stepped in place over PCIe (_fused_server_step_host)
+        cloud = cloud.pin_memory()
     cloud.requires_grad = True
     opt = server_storage.read("optimizer_def")(params=[cloud])
     sched_def = server_storage.read("lr_scheduler_def")

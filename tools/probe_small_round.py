@@ -51,13 +51,18 @@ def main():
     ap.add_argument("--P", type=int, default=199_210)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--borrow-host", type=int, default=1)
+    ap.add_argument("--pinned-cloud", type=int, default=0,
+                    help="a page-locked cloud, as the round driver's init_cloud makes it")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     wrap(A._Ingest, "_put_locked", "put")
     wrap(A._DeviceEntry, "_flush", "flush")
     wrap(A._DeviceEntry, "release", "release")
     wrap(tu, "_fused_server_step_host", "fused_server_step_host")
-    cloud = torch.zeros(a.P, requires_grad=True)
+    cloud = torch.zeros(a.P)
+    if a.pinned_cloud:
+        cloud = cloud.pin_memory()
+    cloud.requires_grad_()
     rounds = []
     for rep in range(a.reps + 3):
         msgs = messages(a.K, a.P, "cpu_run", dev, seed=11 + rep)
@@ -83,7 +88,7 @@ def main():
         if rep >= 3:
             rounds.append((t1 - t0, t2 - t1, t2 - t0))
     med = lambda xs: statistics.median(xs) * 1e6  # noqa: E731
-    out = dict(K=a.K, P=a.P, reps=a.reps,
+    out = dict(K=a.K, P=a.P, reps=a.reps, pinned_cloud=bool(a.pinned_cloud),
                receive_us=med([r[0] for r in rounds]), optimize_us=med([r[1] for r in rounds]),
                round_us=med([r[2] for r in rounds]),
                stages_us_per_call={k: med(v) for k, v in T.items()},
