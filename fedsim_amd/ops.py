@@ -348,7 +348,7 @@ def segment_table(tensors: Sequence[torch.Tensor], device: torch.device):
     if table is None:
         if len(_TABLES) > 64:
             _TABLES.clear()
-        host = torch.tensor(list(key[1]) or [0, 0, 0], dtype=torch.int64).pin_memory()
+        host = torch.tensor(list(key[1]) or [0, 0, 0], dtype=torch.int64, pin_memory=True)
         table = _TABLES[key] = host.to(device, non_blocking=True)
     return table, len(segs), P
 
@@ -644,7 +644,7 @@ def reduce_rows_ref(rows: Sequence[torch.Tensor], weights: Sequence, out: torch.
         raise ValueError("no rows and no acc_in")
     table = row_table_from_ptrs([r.data_ptr() for r in rows], dev) if B else None
     wv = torch.tensor([fl32(w) if wdt == torch.float32 else float(w) for w in weights],
-                      dtype=wdt).pin_memory().to(dev, non_blocking=True) if B else None
+                      dtype=wdt, pin_memory=True).to(dev, non_blocking=True) if B else None
     flags = (FEDAGG_INIT if acc_in is None else 0) | (0 if aligned else FEDAGG_SCALAR)
     rc = _native.load().fedagg_reduce_rows_ref(code, _ptr(table), _ptr(wv), B, P, _ptr(acc_in),
                                                out.data_ptr(), flags, _stream_ptr(dev))
@@ -900,7 +900,7 @@ def row_table(rows: Sequence[torch.Tensor], device: torch.device) -> torch.Tenso
 
 def row_table_from_ptrs(ptrs: Sequence[int], device: torch.device) -> torch.Tensor:
     """row_table of pointers collected beforehand (as rows arrive)."""
-    host = torch.tensor(list(ptrs) or [0], dtype=torch.int64).pin_memory()
+    host = torch.tensor(list(ptrs) or [0], dtype=torch.int64, pin_memory=True)
     return host.to(device, non_blocking=True)
 
 

@@ -94,7 +94,9 @@ _STAGING_SLOTS = 3
 # 1.39-1.41 ms against 1.92-1.98 for four memmoves, 2.0-2.3 for one); at
 # 100 MB four memmoves keep the round at the link (53.2-53.4 GB/s against
 # 43-46 for torch's copy_, whose 16 threads take the host memory bandwidth
-# the concurrent DMA reads from).  "auto" takes each below / from 32 MB.
+# the concurrent DMA reads from; six or eight threads measured no better,
+# profiles/r06w/ab_staging_threads.jsonl).  "auto" takes each below / from
+# 32 MB.
 _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
 # How a page-locked host vector (the caller's, or the staging slot) reaches
 # its slab row: "zero_copy", the pack kernel reading it in place over PCIe
@@ -662,7 +664,7 @@ class _DeviceEntry(_TensorEntry):
                     "reduced (use borrow=False to snapshot it at add time)")
             rows.append(t)
         cur = torch.cuda.current_stream(self.dev)
-        w32 = torch.tensor(self.pending_w, dtype=torch.float32).pin_memory()
+        w32 = torch.tensor(self.pending_w, dtype=torch.float32, pin_memory=True)
         w32 = w32.to(self.dev, non_blocking=True)
         table = ops.row_table_from_ptrs(self.borrowed_ptrs, self.dev)
         # every row passed _borrowable at add: skip the per-row checks
@@ -704,7 +706,7 @@ class _DeviceEntry(_TensorEntry):
             cur.wait_event(self.copy_event)
             self.copy_event = None
         acc_in = self.acc
-        w32 = torch.tensor(self.pending_w, dtype=torch.float32).pin_memory()
+        w32 = torch.tensor(self.pending_w, dtype=torch.float32, pin_memory=True)
         w32 = w32.to(self.dev, non_blocking=True)
         first = self.R - self.tail
         segs = [(self.tail, n)] if n <= first else [(self.tail, first), (0, n - first)]

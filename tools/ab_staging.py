@@ -5,6 +5,8 @@ config-2 host round (K=10 x 1 085 668 handed-over pageable vectors, add x K
 + get_sum, wall clock).
 
 python tools/ab_staging.py [--variants torch,memmove4,memmove1] [--rounds 3]
+(',' or ':' separate the variants; a variant "memmove4+zc" also reads the
+staging slot in place, aggregators._HOST_PACK = "zero_copy")
 """
 import argparse
 import json
@@ -47,8 +49,9 @@ def main():
     torch.cuda.set_device(0)
     vecs = [torch.randn(1_085_668) for _ in range(10)]
     for r in range(a.rounds):
-        for v in a.variants.split(","):
-            A._STAGE_COPY = v
+        for v in a.variants.replace(":", ",").split(","):
+            A._STAGE_COPY, zc = v.split("+")[0], v.endswith("+zc")
+            A._HOST_PACK = "zero_copy" if zc else "auto"
             for P in (int(x) for x in a.P.split(",")):
                 h = bench.h2d_inclusive_leg(_Rk(), P)
                 print(json.dumps({"round": r, "variant": v, "P": P, "h2d_pageable": h["pageable"],
