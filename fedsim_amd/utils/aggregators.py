@@ -94,9 +94,11 @@ _STAGING_SLOTS = 3
 # 1.39-1.41 ms against 1.92-1.98 for four memmoves, 2.0-2.3 for one); at
 # 100 MB four memmoves keep the round at the link (53.2-53.4 GB/s against
 # 43-46 for torch's copy_, whose 16 threads take the host memory bandwidth
-# the concurrent DMA reads from; six or eight threads measured no better,
-# profiles/r06w/ab_staging_threads.jsonl).  "auto" takes each below / from
-# 32 MB.
+# the concurrent DMA reads from).  At 100 MB six threads keep the copy ahead
+# of the 53 GB/s DMA with headroom: over two boxes (profiles/r06w/
+# ab_staging_threads*.jsonl) the pageable round's median is 53.1 GB/s with
+# six threads against 49.5 with four (nine rounds each; eight: no better).
+# "auto" takes torch's copy below 32 MB and six threads from 32 MB.
 _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
 # How a page-locked host vector (the caller's, or the staging slot) reaches
 # its slab row: "zero_copy", the pack kernel reading it in place over PCIe
@@ -122,7 +124,7 @@ def _staging_copy(dst: torch.Tensor, src: torch.Tensor) -> None:
     global _stage_pool
     how = _STAGE_COPY
     if how == "auto":
-        how = "memmove4" if 4 * src.numel() >= _STAGE_SPLIT_MIN else "torch"
+        how = "memmove6" if 4 * src.numel() >= _STAGE_SPLIT_MIN else "torch"
     if how == "torch" or not (src.is_contiguous() and src.dtype == torch.float32):
         dst.copy_(src)
         return
