@@ -137,7 +137,7 @@ def _staging_copy(dst: torch.Tensor, src: torch.Tensor) -> None:
         return
     if _stage_pool is None or _stage_pool._max_workers < n - 1:
         _stage_pool = ThreadPoolExecutor(max_workers=n - 1, thread_name_prefix="fedsim-stage")
-    step = (nbytes // n + 4095) & ~4095
+    step = (-(-nbytes // n) + 4095) & ~4095  # page-rounded, n * step >= nbytes
     futs = [_stage_pool.submit(ctypes.memmove, d + i * step, s + i * step,
                                min(step, nbytes - i * step))
             for i in range(1, n) if i * step < nbytes]

@@ -505,8 +505,10 @@ def test_hand_over_round_scope_releases_tokens():
 
 
 
-@pytest.mark.parametrize("how", ["auto", "torch", "memmove1", "memmove3", "memmove4", "memmove6"])
-@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 3 * 1024 + 5, 1 << 14, (1 << 14) + 3])
+@pytest.mark.parametrize("how", ["auto", "torch", "memmove1", "memmove3", "memmove4", "memmove6",
+                                 "memmove8"])
+@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 3 * 1024 + 5, 1 << 14, (1 << 14) + 3,
+                               6 * 1024 + 1, 12 * 1024 + 1, 6 * 2048 + 2])
 def test_staging_copy_is_exact(monkeypatch, how, n):
     """The ingest worker's staging copy (aggregators._staging_copy) writes
     exactly the source floats for every method, size and thread split
