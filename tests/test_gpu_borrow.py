@@ -515,6 +515,27 @@ def test_host_pack_modes_are_exact(dev, mode, borrow_host, monkeypatch):
                                       bits(ref.reduce(X, w, W=sum(w))))
 
 
+@pytest.mark.parametrize("borrow_host", [False, True])
+def test_split_staging_copy_keeps_the_tail(dev, borrow_host):
+    """From 32 MB the staging copy runs on six memmove threads; at P = 6144m + 1
+    floats the byte count is not a multiple of six pages' worth, and the
+    last chunk must still reach the slot (every column bitwise, the last
+    included)."""
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _STAGE_SPLIT_MIN
+
+    P = 6144 * 1366 + 1
+    assert 4 * P >= _STAGE_SPLIT_MIN
+    K = 3
+    X = V.client_rows("realistic", K, P, 14)
+    w = V.client_weights("fedavg", K, 14)
+    agg = SerialAggregator(borrow=True, borrow_host=borrow_host)
+    for k in range(K):
+        agg.add("p", torch.from_numpy(X[k].copy()), w[k])
+    out = agg.pop("p").numpy()
+    np.testing.assert_array_equal(bits(out), bits(ref.reduce(X, w, W=sum(w))))
+
+
 def test_handed_over_host_rows_are_staged_after_add(dev):
     """borrow_host=True with host vectors (the round driver's aggregator under
     device="cpu"): each handed-over vector is copied into pinned staging and
