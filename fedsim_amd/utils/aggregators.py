@@ -114,6 +114,13 @@ _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
 # below 64 MB and the DMA otherwise.
 _HOST_PACK = os.environ.get("FEDSIM_AMD_HOST_PACK", "auto")
 _ZERO_COPY_MAX = 64 << 20
+# The caller's own pinned vectors from this size on are DMA'd straight from
+# its buffer, the put waiting for the DMA so the caller may reuse it; smaller
+# ones are staged like pageable vectors (a pinned-to-pinned copy, then the
+# put returns): profiles/r06N/plugin_round.jsonl had pinned rounds slower
+# than pageable ones below 32 MB (config 1 0.48 vs 0.36 ms, config 2 K=10
+# 1.46 vs 1.24 ms) and faster at 100 MB (53.0 vs 51.2 GB/s).
+_PINNED_DIRECT_MIN = int(os.environ.get("FEDSIM_AMD_PINNED_DIRECT_MIN", 32 << 20))
 _STAGE_SPLIT_MIN = 32 << 20
 _stage_pool: Optional[ThreadPoolExecutor] = None
 
@@ -275,7 +282,7 @@ class _Ingest(object):
         if self.events[i] is not None:
             self.events[i].synchronize()
         P = src.numel()
-        if src.is_pinned():
+        if src.is_pinned() and 4 * P >= _PINNED_DIRECT_MIN:
             host = src  # DMA straight from the caller's pinned buffer
         else:
             host = self._slot(self.hbufs, i, P, pin_memory=True)
