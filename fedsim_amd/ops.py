@@ -693,7 +693,10 @@ def feddyn_sgd(avg: torch.Tensor, cloud: torch.Tensor, h: torch.Tensor, ratio: f
 def host_mapped(t: torch.Tensor) -> bool:
     """Whether ``t`` is page-locked host memory the GPU reaches at its own
     address (fedagg_host_mapped: torch's pin_memory on this platform), so a
-    kernel can read and write it in place over PCIe."""
+    kernel can read and write it in place over PCIe.  hipHostMalloc maps
+    such memory into the address space of every GPU in the system
+    (hip_runtime_api.h), so this holds for whichever device a kernel runs on
+    (torch's host allocator shares its blocks across devices)."""
     if not isinstance(t, torch.Tensor) or t.device.type != "cpu" or not t.is_pinned():
         return False
     nbytes = t.numel() * t.element_size()
