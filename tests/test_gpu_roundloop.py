@@ -83,6 +83,10 @@ def test_round_loop_matches_reference(run, device, arrays):
             continue
         t = st.read(name)
         assert t.device.type == device
+        if name == "cloud_params" and device == "cpu":
+            # init_cloud pins the host cloud: the step kernel updates it in
+            # place over PCIe (training/utils._fused_server_step_host)
+            assert t.is_pinned()
         got, want = t.detach().cpu().numpy(), arrays[key]
         if exact:
             np.testing.assert_array_equal(bits(got), bits(want))
