@@ -114,6 +114,11 @@ _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
 # below 64 MB and the DMA otherwise.
 _HOST_PACK = os.environ.get("FEDSIM_AMD_HOST_PACK", "auto")
 _ZERO_COPY_MAX = 64 << 20
+# The ingest ring's DMAs and packs on two streams (the DMA engine does not
+# idle while a pack runs), and the caller's handed-over pinned vectors
+# checked at the reduction instead of after each DMA (the worker does not
+# idle between DMAs); "0" restores one stream and per-put waits (A/B).
+_INGEST_OVERLAP = os.environ.get("FEDSIM_AMD_INGEST_OVERLAP", "1") == "1"
 # The caller's own pinned vectors from this size on are DMA'd straight from
 # its buffer, the put waiting for the DMA so the caller may reuse it; smaller
 # ones are staged like pageable vectors (a pinned-to-pinned copy, then the
@@ -227,14 +232,16 @@ class _Ingest(object):
     trains instead of between the two clients (tools/bench_host_rounds.py:
     0.2-1.5 ms per client on the critical path otherwise).  A handed-over
     vector changed in place (an in-place torch op: its version counter) from
-    ``add`` until its copy has completed -- the copy into staging, or for
-    a pinned source the DMA straight from it -- is caught: the counter is
-    checked before and after the copy, and the error is raised at the
-    round's reduction.  A change after that point cannot alter the row."""
+    ``add`` until its copy has completed is caught and raised at the round's
+    reduction: a staged vector's counter is checked before and after its copy
+    into staging (a later change cannot alter the row); a pinned vector DMA'd
+    straight from the caller's buffer is checked when the reduction waits for
+    that DMA, so any change before then raises, as for a borrowed HBM row."""
 
     def __init__(self, dev: torch.device, nslots: int = _STAGING_SLOTS):
         self.dev = dev
-        self.stream = torch.cuda.Stream(device=dev)
+        self.stream = torch.cuda.Stream(device=dev)  # DMAs into the device slots
+        self.pack_stream = torch.cuda.Stream(device=dev)  # packs into the slab rows
         self.hbufs: List[Optional[torch.Tensor]] = [None] * nslots
         self.dbufs: List[Optional[torch.Tensor]] = [None] * nslots
         self.events: List[Optional[torch.cuda.Event]] = [None] * nslots
@@ -243,6 +250,11 @@ class _Ingest(object):
                                        initializer=torch.cuda.set_device, initargs=(dev,))
         self.lock = threading.Lock()
         self.last: Optional[Future] = None  # the latest asynchronous put
+
+    def drain(self) -> None:
+        """Every DMA and pack issued so far has completed."""
+        self.stream.synchronize()
+        self.pack_stream.synchronize()
 
     def put(self, src: torch.Tensor, Xb: torch.Tensor, r: int, wait_event=None):
         if self.last is not None:
@@ -282,7 +294,8 @@ class _Ingest(object):
         if self.events[i] is not None:
             self.events[i].synchronize()
         P = src.numel()
-        if src.is_pinned() and 4 * P >= _PINNED_DIRECT_MIN:
+        direct = src.is_pinned() and 4 * P >= _PINNED_DIRECT_MIN
+        if direct:
             host = src  # DMA straight from the caller's pinned buffer
         else:
             host = self._slot(self.hbufs, i, P, pin_memory=True)
@@ -294,22 +307,32 @@ class _Ingest(object):
             _staging_copy(host, src)
             self._check_version(src, version)  # not changed while it was copied
         packed = host  # the pack kernel reads it in place over PCIe
+        pack_stream = self.pack_stream if _INGEST_OVERLAP else self.stream
         if _HOST_PACK == "dma" or (_HOST_PACK == "auto" and (
-                host is src or 4 * P >= _ZERO_COPY_MAX)):
-            # a DMA into a device slot, then the HBM pack
+                direct or 4 * P >= _ZERO_COPY_MAX)):
+            # a DMA into a device slot, then the HBM pack -- on its own stream,
+            # so the next vector's DMA does not queue behind this pack
             packed = self._slot(self.dbufs, i, P, device=self.dev)
             with torch.cuda.stream(self.stream):
                 packed.copy_(host, non_blocking=True)
+            if pack_stream is not self.stream:
+                pack_stream.wait_stream(self.stream)
         if wait_event is not None:
-            self.stream.wait_event(wait_event)
-        ops.pack_row(packed, Xb, r, stream=self.stream)
+            pack_stream.wait_event(wait_event)
+        ops.pack_row(packed, Xb, r, stream=pack_stream)
         ev = torch.cuda.Event()
-        ev.record(self.stream)
+        ev.record(pack_stream)
         self.events[i] = ev
-        if host is src:
+        if direct:
+            if version is not None and _INGEST_OVERLAP:
+                # handed over: the worker moves on to the next vector; the
+                # entry waits for this copy and checks the version at the
+                # reduction (_DeviceEntry._copies_issued), where a change
+                # made in place before the round is reduced raises as for a
+                # borrowed HBM row (utils/handover.py)
+                return ev, (src, version, ev)
             # the snapshot is complete once the DMA is: the caller may reuse
-            # its pinned buffer after add returns (a handed-over one: checked
-            # once the DMA has read it, on the worker thread)
+            # its pinned buffer after add returns
             ev.synchronize()
             self._check_version(src, version)
         return ev
@@ -493,12 +516,23 @@ class _DeviceEntry(_TensorEntry):
             futs, self.staging = self.staging, []
             _wait_futures(futs)
             for f in futs:
-                if f.exception() is not None:
+                err = f.exception()
+                if err is None and isinstance(f.result(), tuple):
+                    # a handed-over pinned vector DMA'd straight from the
+                    # caller's buffer: unchanged until its copy completed?
+                    src, version, done = f.result()[1]
+                    done.synchronize()
+                    try:
+                        _Ingest._check_version(src, version)
+                    except RuntimeError as e:
+                        err = e
+                if err is not None:
                     self.copy_event = None
-                    self.failed = f.exception()
+                    self.failed = err
                     raise self.failed
         if isinstance(self.copy_event, Future):
-            self.copy_event = self.copy_event.result()
+            res = self.copy_event.result()
+            self.copy_event = res[0] if isinstance(res, tuple) else res
 
     def _alloc(self, rows: int) -> None:
         self._copies_issued()
@@ -582,7 +616,7 @@ class _DeviceEntry(_TensorEntry):
             self._copies_issued()
         except BaseException:  # noqa: BLE001 -- the entry's own calls raise it
             self.copy_event = None
-            self.agg._ingest(self.dev).stream.synchronize()
+            self.agg._ingest(self.dev).drain()
         if self.copy_event is not None:  # the slab is read by the copy stream until then
             self.copy_event.synchronize()
             self.copy_event = None

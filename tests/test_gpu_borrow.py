@@ -536,6 +536,33 @@ def test_split_staging_copy_keeps_the_tail(dev, borrow_host):
     np.testing.assert_array_equal(bits(out), bits(ref.reduce(X, w, W=sum(w))))
 
 
+def test_handed_over_large_pinned_rows_are_checked_at_the_reduction(dev):
+    """From 32 MB a handed-over pinned vector is DMA'd straight from the
+    caller's buffer and the ingest worker does not wait for the DMA: the
+    reduction does, and checks the vector's version there -- unchanged rows
+    reduce bit for bit, a row changed in place before the round is reduced
+    (even after its DMA completed) raises, as for a borrowed HBM row."""
+    from fedsim_amd.utils import SerialAggregator
+    from fedsim_amd.utils.aggregators import _PINNED_DIRECT_MIN
+
+    P = _PINNED_DIRECT_MIN // 4 + 5
+    K = 3
+    X = V.client_rows("realistic", K, P, 15)
+    w = V.client_weights("fedavg", K, 15)
+    rows = [torch.from_numpy(X[k].copy()).pin_memory() for k in range(K)]
+    agg = SerialAggregator(borrow=True, borrow_host=True)
+    for k in range(K):
+        agg.add("p", rows[k], w[k])
+    np.testing.assert_array_equal(bits(agg.pop("p").numpy()), bits(ref.reduce(X, w, W=sum(w))))
+    agg = SerialAggregator(borrow=True, borrow_host=True)
+    for k in range(K):
+        agg.add("p", rows[k], w[k])
+    torch.cuda.synchronize()  # every DMA has completed
+    rows[1].mul_(2)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        agg.pop("p")
+
+
 def test_handed_over_host_rows_are_staged_after_add(dev):
     """borrow_host=True with host vectors (the round driver's aggregator under
     device="cpu"): each handed-over vector is copied into pinned staging and

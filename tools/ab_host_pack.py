@@ -49,6 +49,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--h2d-only", action="store_true")
+    ap.add_argument("--overlap-ab", action="store_true",
+                    help="A/B aggregators._INGEST_OVERLAP instead (off = 'dma' column, "
+                         "on = 'zero_copy' column), on the host-vector rounds")
     ap.add_argument("--step-ab", action="store_true",
                     help="A/B the host server step (training/utils._HOST_STEP) instead, "
                          "on the cloud-on-host rounds")
@@ -63,15 +66,23 @@ def main():
              ("cfg2_K1000_host_pageable", 1000, 1_085_668, "host_pageable", 2)]
     if a.step_ab:
         cases = [c for c in cases if c[3] == "cpu_run"]
+    if a.overlap_ab:
+        cases = [("cfg2_K1000_host_pinned", 1000, 1_085_668, "host_pinned", 2),
+                 ("cfg2_K1000_host_pageable", 1000, 1_085_668, "host_pageable", 2)]
+
+    def set_mode(m):
+        if a.step_ab:
+            U._HOST_STEP = m
+        elif a.overlap_ab:
+            A._INGEST_OVERLAP = m == "zero_copy"
+        else:
+            A._HOST_PACK = m
     for name, K, P, where, n in ([] if a.h2d_only else cases):
         times = {m: [] for m in MODES}
         outs = {}
         for rep in range(n + 1):
             for m in MODES:
-                if a.step_ab:
-                    U._HOST_STEP = m
-                else:
-                    A._HOST_PACK = m
+                set_mode(m)
                 t, c = plugin_round(K, P, where, dev)
                 if rep:
                     times[m].append(t)
@@ -79,7 +90,8 @@ def main():
         same = torch.equal(outs["dma"].view(torch.int32), outs["zero_copy"].view(torch.int32))
         res[name] = {m: round(statistics.median(v) * 1e3, 3) for m, v in times.items()}
         res[name].update(unit="ms per round", bitwise_equal=same,
-                         toggled="_HOST_STEP" if a.step_ab else "_HOST_PACK")
+                         toggled="_HOST_STEP" if a.step_ab else
+                         "_INGEST_OVERLAP" if a.overlap_ab else "_HOST_PACK")
         print(json.dumps({name: res[name]}), flush=True)
     for P, pinned in [(int(p), pin) for p in a.h2d_P.split(":") for pin in (True, False)
                       if not a.step_ab]:
@@ -92,7 +104,7 @@ def main():
         outs = {}
         for rep in range(a.reps + 1):
             for m in MODES:
-                A._HOST_PACK = m
+                set_mode(m)
                 t, out = h2d_round(pool, K, w, pinned)
                 if rep:
                     times[m].append(t)
@@ -100,10 +112,11 @@ def main():
         same = torch.equal(outs["dma"].view(torch.int32), outs["zero_copy"].view(torch.int32))
         name = f"h2d_P{P}_K{K}_" + ("pinned" if pinned else "pageable")
         res[name] = {m: round(4.0 * K * P / statistics.median(v) / 1e9, 2) for m, v in times.items()}
-        res[name].update(unit="GB/s", bitwise_equal=same)
+        res[name].update(unit="GB/s", bitwise_equal=same,
+                         toggled="_INGEST_OVERLAP" if a.overlap_ab else "_HOST_PACK")
         print(json.dumps({name: res[name]}), flush=True)
         del pool, outs
-    A._HOST_PACK, U._HOST_STEP = "auto", "zero_copy"
+    A._HOST_PACK, U._HOST_STEP, A._INGEST_OVERLAP = "auto", "zero_copy", True
     print(json.dumps({"all": res}), flush=True)
 
 
