@@ -130,6 +130,20 @@ _STAGE_SPLIT_MIN = 32 << 20
 _stage_pool: Optional[ThreadPoolExecutor] = None
 
 
+def _host_route(pinned: bool, nbytes: int):
+    """(direct, dma) for a host vector of ``nbytes`` reaching its slab row:
+    ``direct`` -- DMA'd straight from the caller's pinned buffer rather than
+    staged (_PINNED_DIRECT_MIN); ``dma`` -- through a device slot and the HBM
+    pack rather than the pack kernel reading the page-locked vector in place
+    (_HOST_PACK, _ZERO_COPY_MAX)."""
+    direct = pinned and nbytes >= _PINNED_DIRECT_MIN
+    if _HOST_PACK == "dma":
+        return direct, True
+    if _HOST_PACK == "zero_copy":
+        return direct, False
+    return direct, direct or nbytes >= _ZERO_COPY_MAX
+
+
 def _staging_copy(dst: torch.Tensor, src: torch.Tensor) -> None:
     """dst.copy_(src) for a pinned fp32 slot and a source of its size, by
     _STAGE_COPY's method."""
@@ -294,7 +308,7 @@ class _Ingest(object):
         if self.events[i] is not None:
             self.events[i].synchronize()
         P = src.numel()
-        direct = src.is_pinned() and 4 * P >= _PINNED_DIRECT_MIN
+        direct, dma = _host_route(src.is_pinned(), 4 * P)
         if direct:
             host = src  # DMA straight from the caller's pinned buffer
         else:
@@ -308,8 +322,7 @@ class _Ingest(object):
             self._check_version(src, version)  # not changed while it was copied
         packed = host  # the pack kernel reads it in place over PCIe
         pack_stream = self.pack_stream if _INGEST_OVERLAP else self.stream
-        if _HOST_PACK == "dma" or (_HOST_PACK == "auto" and (
-                direct or 4 * P >= _ZERO_COPY_MAX)):
+        if dma:
             # a DMA into a device slot, then the HBM pack -- on its own stream,
             # so the next vector's DMA does not queue behind this pack
             packed = self._slot(self.dbufs, i, P, device=self.dev)

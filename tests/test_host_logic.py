@@ -407,6 +407,28 @@ def test_changed_client_storage_keys():
     assert _removed_keys(st, state) == ["same"]
 
 
+def test_host_route_policy(monkeypatch):
+    """How a host vector reaches its slab row (aggregators._host_route):
+    pageable vectors are staged, and so are pinned ones below 32 MB; staged
+    vectors below 64 MB are read in place by the pack kernel, larger ones and
+    the caller's own pinned vectors from 32 MB go through a DMA; the
+    _HOST_PACK switch forces either path (the A/B runs)."""
+    from fedsim_amd.utils import aggregators as A
+
+    MB = 1 << 20
+    monkeypatch.setattr(A, "_HOST_PACK", "auto")
+    assert A._host_route(False, 4 * MB) == (False, False)
+    assert A._host_route(True, 4 * MB) == (False, False)
+    assert A._host_route(False, 40 * MB) == (False, False)
+    assert A._host_route(True, 40 * MB) == (True, True)
+    assert A._host_route(False, 100 * MB) == (False, True)
+    assert A._host_route(True, 100 * MB) == (True, True)
+    monkeypatch.setattr(A, "_HOST_PACK", "dma")
+    assert A._host_route(False, 4 * MB) == (False, True)
+    monkeypatch.setattr(A, "_HOST_PACK", "zero_copy")
+    assert A._host_route(True, 100 * MB) == (True, False)
+
+
 def test_server_step_device_rule():
     """A ServerStep runs on one device: its operands live there, or are
     page-locked host memory the GPU reaches at its own address
