@@ -130,17 +130,21 @@ _STAGE_SPLIT_MIN = 32 << 20
 _stage_pool: Optional[ThreadPoolExecutor] = None
 
 
-def _host_route(pinned: bool, nbytes: int):
+def _host_route(pinned: bool, nbytes: int, odd: bool = False):
     """(direct, dma) for a host vector of ``nbytes`` reaching its slab row:
     ``direct`` -- DMA'd straight from the caller's pinned buffer rather than
     staged (_PINNED_DIRECT_MIN); ``dma`` -- through a device slot and the HBM
     pack rather than the pack kernel reading the page-locked vector in place
-    (_HOST_PACK, _ZERO_COPY_MAX)."""
+    (_HOST_PACK, _ZERO_COPY_MAX).  "mixed" alternates the two for staged
+    vectors (``odd``: every second one), so the DMA engine and the pack
+    kernel share the link."""
     direct = pinned and nbytes >= _PINNED_DIRECT_MIN
     if _HOST_PACK == "dma":
         return direct, True
     if _HOST_PACK == "zero_copy":
         return direct, False
+    if _HOST_PACK == "mixed":
+        return direct, direct or nbytes >= _ZERO_COPY_MAX or odd
     return direct, direct or nbytes >= _ZERO_COPY_MAX
 
 
@@ -308,7 +312,7 @@ class _Ingest(object):
         if self.events[i] is not None:
             self.events[i].synchronize()
         P = src.numel()
-        direct, dma = _host_route(src.is_pinned(), 4 * P)
+        direct, dma = _host_route(src.is_pinned(), 4 * P, odd=bool(self.i & 1))
         if direct:
             host = src  # DMA straight from the caller's pinned buffer
         else:

@@ -49,6 +49,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--h2d-only", action="store_true")
+    ap.add_argument("--pack-modes", default="dma:zero_copy",
+                    help="the two _HOST_PACK values compared (':'-separated)")
     ap.add_argument("--overlap-ab", action="store_true",
                     help="A/B aggregators._INGEST_OVERLAP instead (off = 'dma' column, "
                          "on = 'zero_copy' column), on the host-vector rounds")
@@ -57,6 +59,9 @@ def main():
                          "on the cloud-on-host rounds")
     ap.add_argument("--h2d-P", default="25000000", help="vector sizes, separated by :")
     a = ap.parse_args()
+    global MODES
+    if not (a.step_ab or a.overlap_ab):
+        MODES = tuple(a.pack_modes.split(":"))
     dev = torch.device("cuda:0")
     res = {}
     cases = [("cfg1_cpu_run", 5, 199_210, "cpu_run", 30),
@@ -72,9 +77,9 @@ def main():
 
     def set_mode(m):
         if a.step_ab:
-            U._HOST_STEP = m
+            U._HOST_STEP = "zero_copy" if m == MODES[1] else "dma"
         elif a.overlap_ab:
-            A._INGEST_OVERLAP = m == "zero_copy"
+            A._INGEST_OVERLAP = m == MODES[1]
         else:
             A._HOST_PACK = m
     for name, K, P, where, n in ([] if a.h2d_only else cases):
@@ -87,7 +92,7 @@ def main():
                 if rep:
                     times[m].append(t)
                 outs[m] = c
-        same = torch.equal(outs["dma"].view(torch.int32), outs["zero_copy"].view(torch.int32))
+        same = torch.equal(outs[MODES[0]].view(torch.int32), outs[MODES[1]].view(torch.int32))
         res[name] = {m: round(statistics.median(v) * 1e3, 3) for m, v in times.items()}
         res[name].update(unit="ms per round", bitwise_equal=same,
                          toggled="_HOST_STEP" if a.step_ab else
@@ -109,7 +114,7 @@ def main():
                 if rep:
                     times[m].append(t)
                 outs[m] = out
-        same = torch.equal(outs["dma"].view(torch.int32), outs["zero_copy"].view(torch.int32))
+        same = torch.equal(outs[MODES[0]].view(torch.int32), outs[MODES[1]].view(torch.int32))
         name = f"h2d_P{P}_K{K}_" + ("pinned" if pinned else "pageable")
         res[name] = {m: round(4.0 * K * P / statistics.median(v) / 1e9, 2) for m, v in times.items()}
         res[name].update(unit="GB/s", bitwise_equal=same,
