@@ -111,9 +111,16 @@ _STAGE_COPY = os.environ.get("FEDSIM_AMD_STAGE_COPY", "auto")
 # noise at 100 MB; for the caller's own pinned vectors, whose put waits for
 # the copy, the DMA engine wins (4.3 / 32 / 100 MB: 36.3 / 51.2 / 52.5 vs
 # 31.9 / 47.7 / 50.9 GB/s).  "auto" takes the kernel for staged vectors
-# below 64 MB and the DMA otherwise.
+# below 2 MB, alternates the two from 2 MB (_MIXED_MIN) and takes the DMA
+# from 64 MB and for the caller's own pinned vectors.
 _HOST_PACK = os.environ.get("FEDSIM_AMD_HOST_PACK", "auto")
 _ZERO_COPY_MAX = 64 << 20
+# From 2 MB "auto" alternates the two routes per staged vector, so the DMA
+# engine and the pack kernel share the link (profiles/r06w/
+# ab_host_pack_mixed.jsonl, against the kernel alone: config 2 K=1000 host
+# rounds 104.4 vs 112.0 ms, 4.3 MB host->host rounds 39.9 / 40.4 vs 36.3 /
+# 35.8 GB/s pinned / pageable; at 0.8 MB, config 1, it loses: 0.38 vs 0.34 ms).
+_MIXED_MIN = 2 << 20
 # The ingest ring's DMAs and packs on two streams (the DMA engine does not
 # idle while a pack runs), and the caller's handed-over pinned vectors
 # checked at the reduction instead of after each DMA (the worker does not
@@ -145,7 +152,7 @@ def _host_route(pinned: bool, nbytes: int, odd: bool = False):
         return direct, False
     if _HOST_PACK == "mixed":
         return direct, direct or nbytes >= _ZERO_COPY_MAX or odd
-    return direct, direct or nbytes >= _ZERO_COPY_MAX
+    return direct, direct or nbytes >= _ZERO_COPY_MAX or (nbytes >= _MIXED_MIN and odd)
 
 
 def _staging_copy(dst: torch.Tensor, src: torch.Tensor) -> None:

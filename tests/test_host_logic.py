@@ -410,9 +410,10 @@ def test_changed_client_storage_keys():
 def test_host_route_policy(monkeypatch):
     """How a host vector reaches its slab row (aggregators._host_route):
     pageable vectors are staged, and so are pinned ones below 32 MB; staged
-    vectors below 64 MB are read in place by the pack kernel, larger ones and
-    the caller's own pinned vectors from 32 MB go through a DMA; the
-    _HOST_PACK switch forces either path (the A/B runs)."""
+    vectors below 2 MB are read in place by the pack kernel, from 2 MB every
+    second one goes through a DMA instead, larger ones (64 MB) and the
+    caller's own pinned vectors from 32 MB always do; the _HOST_PACK switch
+    forces either path (the A/B runs)."""
     from fedsim_amd.utils import aggregators as A
 
     MB = 1 << 20
@@ -423,6 +424,10 @@ def test_host_route_policy(monkeypatch):
     assert A._host_route(True, 40 * MB) == (True, True)
     assert A._host_route(False, 100 * MB) == (False, True)
     assert A._host_route(True, 100 * MB) == (True, True)
+    # from 2 MB every second staged vector takes the DMA (the link shared)
+    assert A._host_route(False, 4 * MB, odd=True) == (False, True)
+    assert A._host_route(True, 4 * MB, odd=True) == (False, True)
+    assert A._host_route(False, MB, odd=True) == (False, False)
     monkeypatch.setattr(A, "_HOST_PACK", "dma")
     assert A._host_route(False, 4 * MB) == (False, True)
     monkeypatch.setattr(A, "_HOST_PACK", "zero_copy")
