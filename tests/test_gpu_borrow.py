@@ -483,7 +483,7 @@ def test_driver_borrows_by_hand_over_token(keep_view, dev, monkeypatch):
     assert all(decisions) if not keep_view else not any(decisions)
 
 
-@pytest.mark.parametrize("mode", ["auto", "zero_copy", "dma"])
+@pytest.mark.parametrize("mode", ["auto", "zero_copy", "dma", "mixed"])
 @pytest.mark.parametrize("borrow_host", [False, True])
 def test_host_pack_modes_are_exact(dev, mode, borrow_host, monkeypatch):
     """Host vectors reach their slab rows either through the pack kernel
