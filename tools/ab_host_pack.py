@@ -49,6 +49,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--h2d-only", action="store_true")
+    ap.add_argument("--slots-ab", default="",
+                    help="A/B the ingest ring's staging slots instead, e.g. 3:5 (host rounds)")
     ap.add_argument("--pack-modes", default="dma:zero_copy",
                     help="the two _HOST_PACK values compared (':'-separated)")
     ap.add_argument("--overlap-ab", action="store_true",
@@ -60,9 +62,13 @@ def main():
     ap.add_argument("--h2d-P", default="25000000", help="vector sizes, separated by :")
     a = ap.parse_args()
     global MODES
-    if not (a.step_ab or a.overlap_ab):
-        MODES = tuple(a.pack_modes.split(":"))
     dev = torch.device("cuda:0")
+    rings = {}
+    if a.slots_ab:
+        MODES = tuple(a.slots_ab.split(":"))
+        rings = {m: A._Ingest(dev, nslots=int(m)) for m in MODES}
+    elif not (a.step_ab or a.overlap_ab):
+        MODES = tuple(a.pack_modes.split(":"))
     res = {}
     cases = [("cfg1_cpu_run", 5, 199_210, "cpu_run", 30),
              ("cfg1_host_pageable", 5, 199_210, "host_pageable", 30),
@@ -71,12 +77,14 @@ def main():
              ("cfg2_K1000_host_pageable", 1000, 1_085_668, "host_pageable", 2)]
     if a.step_ab:
         cases = [c for c in cases if c[3] == "cpu_run"]
-    if a.overlap_ab:
+    if a.overlap_ab or a.slots_ab:
         cases = [("cfg2_K1000_host_pinned", 1000, 1_085_668, "host_pinned", 2),
                  ("cfg2_K1000_host_pageable", 1000, 1_085_668, "host_pageable", 2)]
 
     def set_mode(m):
-        if a.step_ab:
+        if rings:
+            A._INGESTS[dev] = rings[m]
+        elif a.step_ab:
             U._HOST_STEP = "zero_copy" if m == MODES[1] else "dma"
         elif a.overlap_ab:
             A._INGEST_OVERLAP = m == MODES[1]
@@ -95,7 +103,7 @@ def main():
         same = torch.equal(outs[MODES[0]].view(torch.int32), outs[MODES[1]].view(torch.int32))
         res[name] = {m: round(statistics.median(v) * 1e3, 3) for m, v in times.items()}
         res[name].update(unit="ms per round", bitwise_equal=same,
-                         toggled="_HOST_STEP" if a.step_ab else
+                         toggled="staging slots" if rings else "_HOST_STEP" if a.step_ab else
                          "_INGEST_OVERLAP" if a.overlap_ab else "_HOST_PACK")
         print(json.dumps({name: res[name]}), flush=True)
     for P, pinned in [(int(p), pin) for p in a.h2d_P.split(":") for pin in (True, False)
@@ -118,7 +126,8 @@ def main():
         name = f"h2d_P{P}_K{K}_" + ("pinned" if pinned else "pageable")
         res[name] = {m: round(4.0 * K * P / statistics.median(v) / 1e9, 2) for m, v in times.items()}
         res[name].update(unit="GB/s", bitwise_equal=same,
-                         toggled="_INGEST_OVERLAP" if a.overlap_ab else "_HOST_PACK")
+                         toggled="staging slots" if rings else
+                         "_INGEST_OVERLAP" if a.overlap_ab else "_HOST_PACK")
         print(json.dumps({name: res[name]}), flush=True)
         del pool, outs
     A._HOST_PACK, U._HOST_STEP, A._INGEST_OVERLAP = "auto", "zero_copy", True
