@@ -85,7 +85,12 @@ def _fl32(x) -> float:
     """fl32(x) as a Python float: ATen's rounding of a Python scalar weight
     (round to nearest even), the same as float(np.float32(x))."""
     return _F32.unpack(_F32.pack(x))[0]
-_STAGING_SLOTS = 3
+# Staging slots of the ingest ring (pinned host + device buffers of one
+# vector each): five keep a DMA, a pack kernel and the next staging copy in
+# flight together -- against three, config 2 K=1000 host rounds 100.9 vs
+# 106.4 ms, 16 MB host->host rounds 47.0-47.1 vs 45.0-45.9 GB/s, 100 MB
+# +0.5 % (profiles/r06w/ab_staging_slots.jsonl).
+_STAGING_SLOTS = 5
 
 # How the ingest worker copies a handed-over pageable vector into pinned
 # staging: "auto", "torch" (torch's multi-threaded copy_) or "memmove<N>" (N
